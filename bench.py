@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""bench.py -- Mrays/s of the MI355X path-tracing core (BASELINE.json metric).
+
+A step is one pass of the hot path over one batch: every pixel of a 1920x1080 frame of
+Scenes/bounce.txt (camera 0, recursion 10) gets 256 camera samples (configs[1]).  Scene
+buffers and the fp64 framebuffer stay resident in HBM; only the timed kernels run inside
+the timed region.  One ray = one Scene.RayTrace call (Raytracer.cs:77); one sample = one
+GetColor(x, y) (misses included, FullRaytracer.cs:343).
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): weak
+scaling, each rank renders the same frame with its own disjoint sample range
+(sample_base = (step * N + rank) * spp), and the per-pixel accumulators are summed onto rank
+0 with one RCCL reduce per step (the progressive-refinement merge of FullRaytracer.cs:326-344).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (scene fixture, camera, width, height, spp)
+    "bounce1080": ("bounce.txt", 0, 1920, 1080, 256),
+    "die1080": ("die.txt", 0, 1920, 1080, 1024),
+    "bounce256": ("bounce.txt", 0, 256, 256, 16),
+}
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 vector = fp32 MFMA dense peak
+
+
+def flops_per_ray(info, scene) -> float:
+    """SURVEY.md §8(d) compute view: 20*N_node + 45*N_tri + 30*N_sph (+60 per transformed sphere) + 150."""
+    import raytracercore_amd as rc
+
+    n_tri = sum(1 for p in scene.prims if p.kind == rc.RT_PRIM_TRIANGLE)
+    n_sph = sum(1 for p in scene.prims if p.kind == rc.RT_PRIM_SPHERE)
+    n_xf = sum(1 for p in scene.prims if p.kind == rc.RT_PRIM_SPHERE and p.flags & rc.RT_FLAG_TRANSFORMED)
+    n_pln = sum(1 for p in scene.prims if p.kind == rc.RT_PRIM_PLANE)
+    # brute force tests every primitive on every ray
+    return 45.0 * n_tri + 30.0 * (n_sph + n_pln) + 60.0 * n_xf + 150.0
+
+
+def bytes_per_ray(scene) -> float:
+    """SURVEY.md §8(d) B_ray for brute force (N_node = 0, every primitive tested)."""
+    import raytracercore_amd as rc
+
+    n_tri = sum(1 for p in scene.prims if p.kind == rc.RT_PRIM_TRIANGLE)
+    n_sph = sum(1 for p in scene.prims if p.kind != rc.RT_PRIM_TRIANGLE)
+    n_xf = sum(1 for p in scene.prims if p.kind == rc.RT_PRIM_SPHERE and p.flags & rc.RT_FLAG_TRANSFORMED)
+    return 32 + 16 + 48.0 * n_tri + 16.0 * n_sph + 144.0 * n_xf + 48
+
+
+def cpu_baseline(cfg_name: str, threads: int):
+    """The oracle (C++ fp64 restatement of the reference algorithm) on the host cores, 4 spp."""
+    from oracle.oracle import OracleScene
+    import raytracercore_amd as rc
+
+    scene_file, cam, W, H, _ = CONFIGS[cfg_name]
+    orc = OracleScene.from_file(rc.scene_path(scene_file))
+    orc.set_size(W, H)
+    orc.select_camera(cam)
+    spp = 4 if W * H > 100000 else 16
+    _, n, m, rays, secs, used = orc.render_frame(spp, seed=0, threads=threads)
+    return {
+        "value": round(rays / secs / 1e6, 3),
+        "unit": "Mrays/s",
+        "cores": used,
+        "kind": "port",
+        "sample": f"{scene_file} camera {cam} {W}x{H} x {spp} spp (1 spp per tile pass, FullRaytracer tiling), "
+                  f"{rays} rays in {secs:.2f} s; samples/s {W * H * spp / secs:.4g}; C++ fp64 restatement, "
+                  f"not the C# binary",
+    }
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="bounce1080", choices=sorted(CONFIGS))
+    ap.add_argument("--spp", type=int, default=0, help="override samples per pixel per step")
+    ap.add_argument("--traversal", default="auto", choices=["auto", "brute", "bvh"])
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import raytracercore_amd as rc
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    scene_file, cam, W, H, spp = CONFIGS[args.config]
+    if args.spp > 0:
+        spp = args.spp
+    scene = rc.SceneLoader.from_file(rc.scene_path(scene_file))
+    trav = {"auto": rc.RT_TRAVERSAL_AUTO, "brute": rc.RT_TRAVERSAL_BRUTE, "bvh": rc.RT_TRAVERSAL_BVH}[args.traversal]
+    gpu = rc.GpuRaytracer(scene, cam, device=local, size=(W, H), traversal=trav)
+    info = gpu.info()
+    npix = W * H
+    # frame accumulators (SampleSet[w, h]: sum RGB fp64, samples, misses) and one step's share
+    f_sum = torch.zeros(3 * npix, dtype=torch.float64, device=dev)
+    f_n = torch.zeros(npix, dtype=torch.int32, device=dev)
+    f_m = torch.zeros(npix, dtype=torch.int32, device=dev)
+    d_sum = torch.zeros_like(f_sum)
+    d_n = torch.zeros_like(f_n)
+    d_m = torch.zeros_like(f_m)
+    d_rays = torch.zeros(1, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step(k: int) -> None:
+        base = (k * world + rank) * spp
+        d_sum.zero_()
+        d_n.zero_()
+        d_m.zero_()
+        gpu.render_device(0, 0, W, H, spp, args.seed, base, d_sum.data_ptr(), d_n.data_ptr(), d_m.data_ptr(),
+                          d_rays.data_ptr(), stream)
+
+    def merge() -> None:
+        if world > 1:
+            dist.reduce(d_sum, dst=0)
+            dist.reduce(d_n, dst=0)
+            dist.reduce(d_m, dst=0)
+        if rank == 0:
+            f_sum.add_(d_sum)
+            f_n.add_(d_n)
+            f_m.add_(d_m)
+
+    for k in range(args.warmup):
+        step(k)
+        merge()
+    torch.cuda.synchronize(dev)
+    d_rays.zero_()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for k in range(args.warmup, args.warmup + args.steps):
+        step(k)
+        kernel_ms.append(gpu.last_kernel_ms())  # hipEvent pair around the path kernel
+        merge()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    rays = d_rays.clone()
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        dist.all_reduce(rays, op=dist.ReduceOp.SUM)
+    elapsed = float(elapsed.item())
+    total_rays = int(rays.item())
+    total_samples = npix * spp * args.steps * world
+
+    if rank == 0:
+        n_all = f_n.cpu().numpy().astype(np.int64)
+        m_all = f_m.cpu().numpy().astype(np.int64)
+        expect = spp * (args.steps + args.warmup) * world
+        if not np.all(n_all + m_all == expect):
+            raise SystemExit(f"sample bookkeeping mismatch: {np.unique(n_all + m_all)} != {expect}")
+        my_rays_per_step = total_rays / (args.steps * world)
+        avg_ms = sum(kernel_ms) / len(kernel_ms)
+        fpr = flops_per_ray(info, scene)
+        achieved_tf = fpr * my_rays_per_step / (avg_ms * 1e-3) / 1e12
+        bpr = bytes_per_ray(scene)
+        out = {
+            "metric": "Mrays/sec (primary+secondary) and samples/sec at 1080p, Cornell box",
+            "value": round(total_rays / elapsed / 1e6, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: the reference's own scene file (tests/golden/scenes) with seeded camera samples",
+            "config": {"workload": f"{scene_file} camera {cam} {W}x{H} x {spp} spp per GPU per step",
+                       "traversal": ["auto", "brute", "bvh"][info.traversal], "recursion": scene.params.recursion,
+                       "parallelism": f"sample-sharded x{world}, RCCL reduce per step"},
+            "samples_per_s": round(total_samples / elapsed, 1),
+            "rays_per_sample": round(total_rays / total_samples, 4),
+            "kernel_ms": round(avg_ms, 3),
+            "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                         "note": f"fp32 VALU kernel (no MFMA; the gfx950 fp32 vector and MFMA peaks are both "
+                                 f"157.3 TFLOP/s); {fpr:.0f} algorithmic FLOP per ray (SURVEY 8(d)); HBM view "
+                                 f"(SURVEY B_ray {bpr:.0f} B/ray, scene served from the scalar cache): "
+                                 f"{bpr * my_rays_per_step / (avg_ms * 1e-3) / 1e9:.0f} GB/s"},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(args.config, threads)
+        print(json.dumps(out), flush=True)
+    gpu.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

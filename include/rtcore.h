@@ -1,0 +1,243 @@
+/*
+ * rtcore.h -- C ABI of the MI355X (gfx950) path-tracing core: the drop-in for
+ * RaytracerCore's render worker.
+ *
+ * Reference seam (all paths relative to the reference repository):
+ *   FullRaytracer constructs `Raytracer(this, Scene)` workers
+ *   (RaytracerCore/Raytracing/FullRaytracer.cs:297-302).  Each worker loops
+ *   GetWorkingTile() (FullRaytracer.cs:219-229) -> one sample per pixel of the tile
+ *   into DoubleColor[tile.Width, tile.Height] with DoubleColor.Placeholder marking a
+ *   primary miss (Raytracer.cs:294-330) -> OnTileFinished(tile, samples, elapsed)
+ *   (FullRaytracer.cs:210-214).  The library replaces the body of that loop; the C#
+ *   host keeps Scene / SceneLoader / Camera / SampleSet and calls this ABI through
+ *   P/Invoke.
+ *
+ * Conventions
+ *   - extern "C", cdecl, blittable structs only; every function returns RT_OK (0) or
+ *     a negative rt_status; details via rt_last_error() (thread-local).
+ *   - Host tile buffers use the C# rectangular-array order of DoubleColor[w, h]:
+ *     element (x, y) of a w*h tile lives at offset x*h + y (y fastest),
+ *     as in Raytracer.cs:305,317 and FullRaytracer.cs:328-339.
+ *   - The library owns scene handles and device memory; callers own every output
+ *     buffer and nothing is retained after a call returns.
+ *   - A scene handle is bound to one device and is not re-entrant.
+ */
+#ifndef RTCORE_H
+#define RTCORE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTCORE_ABI_VERSION 1
+
+typedef enum rt_status {
+    RT_OK = 0,
+    RT_ERR_ARG = -1,      /* bad argument (null pointer, bad size, unknown kind)      */
+    RT_ERR_HIP = -2,      /* a HIP runtime call failed                               */
+    RT_ERR_OOM = -3,      /* device or host allocation failed                         */
+    RT_ERR_NCCL = -4,     /* an RCCL call failed                                      */
+    RT_ERR_PARSE = -5,    /* scene text could not be parsed (SceneLoader.cs:417-422) */
+    RT_ERR_NODEVICE = -6, /* no HIP device available                                  */
+    RT_ERR_STATE = -7     /* call out of order (e.g. render before a camera is set)   */
+} rt_status;
+
+/* Vec4D (RaytracerCore/Vectors/Vec4D.cs:16-91): 4 x fp64, 32 B, w=1 points, w=0 directions. */
+typedef struct rt_vec4d { double x, y, z, w; } rt_vec4d;
+
+/* DoubleColor (RaytracerCore/DoubleColor.cs:8-45): 3 x fp64, 24 B.  Placeholder = (-1,-1,-1). */
+typedef struct rt_color { double r, g, b; } rt_color;
+
+typedef enum rt_prim_kind {
+    RT_PRIM_TRIANGLE = 0, /* Primitives/Triangle.cs */
+    RT_PRIM_SPHERE = 1,   /* Primitives/Sphere.cs   */
+    RT_PRIM_PLANE = 2     /* Primitives/Plane.cs    */
+} rt_prim_kind;
+
+typedef enum rt_prim_flags {
+    RT_FLAG_MIRROR = 1,      /* Triangle.Mirror: parallelogram, u,v in [0,1]^2 (Triangle.cs:13-20)    */
+    RT_FLAG_TWOSIDED = 2,    /* Primitive.TwoSided (Primitive.cs:78)                                   */
+    RT_FLAG_INVERT = 4,      /* Primitive.Invert: flips Hit.Inside only (Primitive.cs:60-61)           */
+    RT_FLAG_HASNORMALS = 8,  /* Triangle.HasNormals: per-vertex normals (Triangle.cs:45-52,209-219)   */
+    RT_FLAG_TRANSFORMED = 16 /* Sphere.Transformed: ellipsoid via matrices (Sphere.cs:29-37)           */
+} rt_prim_flags;
+
+/*
+ * One primitive as the C# Scene holds it after SceneLoader finalisation
+ * (SceneLoader.cs:388-413), i.e. after Primitive.Transform.  Derived data
+ * (triangle edges / face normal, bounding boxes, BVH) is computed by the library
+ * with the reference's arithmetic.
+ *   triangle: p[0..2] = Vert0..2.Position (world), n[0..2] = Vert0..2.Normal
+ *   sphere:   p[0] = Center (object space), radius = Radius,
+ *             to_obj = MatrixToObject, to_world = MatrixToWorld, to_normal = MatrixToNormal
+ *             (row-major D00..D33; only read when RT_FLAG_TRANSFORMED is set)
+ *   plane:    p[0] = Normal (unit, w=0), radius = OriginDistance
+ * Materials are the raw backing fields; the library applies the Shininess<=0 gating of
+ * the Specular / Refraction getters (Primitive.cs:111-129).
+ */
+typedef struct rt_prim {
+    int32_t kind;
+    int32_t flags;
+    rt_vec4d p[3];
+    rt_vec4d n[3];
+    double radius;
+    double to_obj[16];
+    double to_world[16];
+    double to_normal[16];
+    rt_color emission, diffuse, specular, refraction;
+    double shininess;
+    double refractive_index;
+} rt_prim;
+
+typedef enum rt_camera_kind {
+    RT_CAMERA_FRUSTUM = 0, /* Cameras/FrustumCamera.cs */
+    RT_CAMERA_ORTHO = 1    /* Cameras/OrthoCamera.cs   */
+} rt_camera_kind;
+
+/*
+ * The public fields of Camera (Cameras/Camera.cs:10-27) before InitRender.  The library
+ * runs InitRender(width, height) itself (Camera.cs:54-63, FrustumCamera.cs:24-31,
+ * OrthoCamera.cs:22-31) with the reference's arithmetic.
+ */
+typedef struct rt_camera {
+    int32_t kind;
+    int32_t reserved;
+    rt_vec4d position, look_at, up;
+    double fov_y;     /* FrustumCamera.fovY, radians                   */
+    double size_mult; /* OrthoCamera.sizeMult                          */
+    double image_plane, dof_amount, focal_length;
+} rt_camera;
+
+/* Scene-wide fields read on the hot path (Scene.cs:16-35). */
+typedef struct rt_scene_params {
+    int32_t width, height; /* Scene.Width / Height: the whole frame                        */
+    int32_t recursion;     /* Scene.Recursion (default 3)                                  */
+    int32_t debug_geom;    /* Scene.DebugGeom                                              */
+    double air_ior;        /* Scene.AirRefractiveIndex (default 1.000293)                  */
+    rt_color ambient;      /* Scene.AmbientRGB; (-1,-1,-1) = "ambient miss"                */
+} rt_scene_params;
+
+typedef struct rt_scene rt_scene; /* opaque */
+
+/* Traversal strategy of the path-tracing kernel. */
+typedef enum rt_traversal {
+    RT_TRAVERSAL_AUTO = 0,  /* brute force for small scenes, BVH otherwise          */
+    RT_TRAVERSAL_BRUTE = 1, /* every primitive, scene read through the scalar cache */
+    RT_TRAVERSAL_BVH = 2    /* binned-SAH BVH2, per-lane LDS stack                  */
+} rt_traversal;
+
+typedef struct rt_scene_info {
+    int32_t n_prims;
+    int32_t ref_bvh_nodes;   /* nodes of the reference agglomerative BVH (BVH.cs:193-236) */
+    int32_t ref_bvh_depth;
+    int32_t sah_bvh_nodes;   /* nodes of the kernel's BVH2                                */
+    int32_t sah_bvh_depth;
+    int32_t traversal;       /* resolved rt_traversal of the path kernel                  */
+    int32_t device;
+    int32_t reserved;
+    uint64_t device_bytes;   /* scene bytes resident in HBM                               */
+} rt_scene_info;
+
+/* ---------------------------------------------------------------- library ---- */
+int rt_abi_version(void);
+int rt_device_count(void);
+/* Copies the calling thread's last error message (NUL-terminated); returns its length. */
+int rt_last_error(char* buf, int32_t cap);
+
+/* ----------------------------------------------------------------- scenes ---- */
+int rt_scene_create(const rt_scene_params* params, const rt_prim* prims, int32_t n_prims,
+                    int32_t device, rt_scene** out_scene);
+int rt_scene_set_camera(rt_scene* scene, const rt_camera* camera);
+int rt_scene_set_traversal(rt_scene* scene, int32_t traversal);
+int rt_scene_get_info(const rt_scene* scene, rt_scene_info* info);
+void rt_scene_destroy(rt_scene* scene);
+
+/* ------------------------------------------------------- host-buffer renders --- */
+/*
+ * Accumulate spp samples (sample indices sample_base .. sample_base+spp-1) for every
+ * pixel of the tile [x0, x0+w) x [y0, y0+h) into caller buffers laid out x*h + y:
+ *   sum_rgb[i] += sum of non-miss sample colours   (SampleSet.AddSample, SampleSet.cs:32-36)
+ *   samples[i] += non-miss samples, misses[i] += misses (SampleSet.AddMiss, :41-44)
+ * rays_out (may be NULL) receives the number of Scene.RayTrace-equivalents (Mrays unit).
+ */
+int rt_render_tile(rt_scene* scene, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t spp,
+                   uint64_t seed, uint64_t sample_base, rt_color* sum_rgb, uint32_t* samples,
+                   uint32_t* misses, uint64_t* rays_out);
+
+/*
+ * Exactly Raytracer.Render's one-pass contract (Raytracer.cs:305-320): one sample per
+ * pixel (index sample_index), written (not accumulated) to out[x*h + y];
+ * primary misses are DoubleColor.Placeholder (-1,-1,-1).
+ */
+int rt_render_tile_1spp(rt_scene* scene, int32_t x0, int32_t y0, int32_t w, int32_t h,
+                        uint64_t seed, uint64_t sample_index, rt_color* out);
+
+/*
+ * DebugRaycaster Primitives mode (DebugRaycaster.cs:193-199,241): integer-pixel primary
+ * ray, no jitter / DOF, closest hit by the reference's BVH query in fp64
+ * (Scene.cs:65-111).  ids_out[x*h + y] = Primitive.ID (insertion order) or -1 on a miss.
+ */
+int rt_primary_ids(rt_scene* scene, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t* ids_out);
+
+/* -------------------------------------------------- device-resident renders --- */
+/*
+ * The same work as rt_render_tile on device buffers (framebuffer stays in HBM).
+ * Device layout is row-major over the tile, i = y*w + x, with planar accumulators:
+ *   d_sum    : 3 * w*h doubles, planes R | G | B
+ *   d_samples, d_misses : w*h uint32
+ *   d_rays   : one uint64 counter (added to)
+ * `stream` is a hipStream_t (NULL = default stream).  Asynchronous: returns after launch.
+ */
+int rt_render_device(rt_scene* scene, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t spp,
+                     uint64_t seed, uint64_t sample_base, double* d_sum, uint32_t* d_samples,
+                     uint32_t* d_misses, unsigned long long* d_rays, void* stream);
+
+/* Device-side DebugRaycaster Primitives pass: d_ids[y*w + x].  Asynchronous. */
+int rt_primary_ids_device(rt_scene* scene, int32_t x0, int32_t y0, int32_t w, int32_t h,
+                          int32_t* d_ids, void* stream);
+
+/* Duration in ms of the last path-tracing kernel launched on this scene (hipEvent pair). */
+int rt_last_kernel_ms(rt_scene* scene, float* ms);
+
+/* ------------------------------------------------------------- multi-GPU ---- */
+/*
+ * Whole frame on n_gpus devices of this process: rows are dealt to devices in
+ * interleaved 16-row bands, each device renders its bands, and an RCCL gather over xGMI
+ * assembles the accumulators on device 0, which are copied to the caller's buffers in
+ * the frame's x*height + y order.
+ */
+int rt_render_frame_multi(const rt_scene_params* params, const rt_prim* prims, int32_t n_prims,
+                          const rt_camera* camera, int32_t n_gpus, int32_t spp, uint64_t seed,
+                          rt_color* sum_rgb, uint32_t* samples, uint32_t* misses, uint64_t* rays_out);
+
+/* ------------------------------------------------------------- scene text ---- */
+/*
+ * SceneLoader.FromFile restatement (SceneLoader.cs:112-440): parses scene text into
+ * primitives (insertion order = Primitive.ID), cameras and scene params.  Two-call
+ * protocol: pass NULL arrays to query the counts, then call again with arrays of at
+ * least that size.  Returns RT_ERR_PARSE with the line number in rt_last_error().
+ */
+int rt_parse_scene(const char* text, rt_scene_params* params, rt_prim* prims, int32_t* n_prims,
+                   rt_camera* cameras, int32_t* n_cameras);
+
+/*
+ * Diagnostic, host only (no device needed): the reference agglomerative BVH the exact pass
+ * uses (BVH.cs:193-236), flattened depth-first.  leaf_order[n] receives primitive indices in
+ * depth-first leaf order; boxes (may be NULL, room for 2n-1 nodes) receives 8 doubles per node
+ * (min xyzw, max xyzw) in pre-order.
+ */
+int rt_ref_bvh_export(const rt_prim* prims, int32_t n_prims, int32_t* leaf_order, double* boxes,
+                      int32_t* n_nodes, int32_t* depth);
+
+/* SampleSet.GetOutput (SampleSet.cs:61-113): tonemap accumulators to ARGB. */
+int32_t rt_sample_output(rt_color sum, uint32_t samples, uint32_t misses, rt_color background,
+                         double background_alpha, double exposure);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RTCORE_H */

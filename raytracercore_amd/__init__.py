@@ -1,0 +1,301 @@
+"""raytracercore_amd -- MI355X (gfx950) path-tracing core behind RaytracerCore's render seam.
+
+The product is ``librtcore_hip.so`` (HIP kernels + the C ABI of ``include/rtcore.h``).  This
+module is the Python host mirror used by the tests and the benchmark: ctypes structs that
+match the ABI, a ``SceneLoader`` over ``rt_parse_scene`` (SceneLoader.FromFile,
+RaytracerCore/SceneLoader.cs:112-440) and a ``GpuRaytracer`` that owns one device scene and
+renders tile passes with the semantics of ``Raytracer.Render`` (Raytracer.cs:294-330).
+
+There is no CPU fallback: if the shared library is missing or no HIP device is present the
+calls raise ``RtError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librtcore_hip.so")
+REPO_ROOT = os.path.dirname(_HERE)
+
+RT_OK = 0
+RT_PRIM_TRIANGLE, RT_PRIM_SPHERE, RT_PRIM_PLANE = 0, 1, 2
+RT_FLAG_MIRROR, RT_FLAG_TWOSIDED, RT_FLAG_INVERT, RT_FLAG_HASNORMALS, RT_FLAG_TRANSFORMED = 1, 2, 4, 8, 16
+RT_CAMERA_FRUSTUM, RT_CAMERA_ORTHO = 0, 1
+RT_TRAVERSAL_AUTO, RT_TRAVERSAL_BRUTE, RT_TRAVERSAL_BVH = 0, 1, 2
+
+
+class RtError(RuntimeError):
+    """A negative rt_status from the library (message from rt_last_error)."""
+
+
+class rt_vec4d(C.Structure):
+    _fields_ = [("x", C.c_double), ("y", C.c_double), ("z", C.c_double), ("w", C.c_double)]
+
+
+class rt_color(C.Structure):
+    _fields_ = [("r", C.c_double), ("g", C.c_double), ("b", C.c_double)]
+
+
+class rt_prim(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32), ("flags", C.c_int32),
+        ("p", rt_vec4d * 3), ("n", rt_vec4d * 3),
+        ("radius", C.c_double),
+        ("to_obj", C.c_double * 16), ("to_world", C.c_double * 16), ("to_normal", C.c_double * 16),
+        ("emission", rt_color), ("diffuse", rt_color), ("specular", rt_color), ("refraction", rt_color),
+        ("shininess", C.c_double), ("refractive_index", C.c_double),
+    ]
+
+
+class rt_camera(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32), ("reserved", C.c_int32),
+        ("position", rt_vec4d), ("look_at", rt_vec4d), ("up", rt_vec4d),
+        ("fov_y", C.c_double), ("size_mult", C.c_double),
+        ("image_plane", C.c_double), ("dof_amount", C.c_double), ("focal_length", C.c_double),
+    ]
+
+
+class rt_scene_params(C.Structure):
+    _fields_ = [
+        ("width", C.c_int32), ("height", C.c_int32), ("recursion", C.c_int32), ("debug_geom", C.c_int32),
+        ("air_ior", C.c_double), ("ambient", rt_color),
+    ]
+
+
+class rt_scene_info(C.Structure):
+    _fields_ = [
+        ("n_prims", C.c_int32), ("ref_bvh_nodes", C.c_int32), ("ref_bvh_depth", C.c_int32),
+        ("sah_bvh_nodes", C.c_int32), ("sah_bvh_depth", C.c_int32), ("traversal", C.c_int32),
+        ("device", C.c_int32), ("reserved", C.c_int32), ("device_bytes", C.c_uint64),
+    ]
+
+
+_lib: Optional[C.CDLL] = None
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    """Load librtcore_hip.so (built by __graft_entry__.build()).  Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RtError(f"{path} is missing: run __graft_entry__.build() (make -C raytracercore_amd/csrc)")
+    # torch-ROCm wheels carry their own HIP runtime; when torch is present it must be loaded
+    # first so that this library binds to the same runtime instance (one HIP runtime per process)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = C.CDLL(path)
+    P = C.POINTER
+    sig = {
+        "rt_abi_version": (C.c_int, []),
+        "rt_device_count": (C.c_int, []),
+        "rt_last_error": (C.c_int, [C.c_char_p, C.c_int32]),
+        "rt_scene_create": (C.c_int, [P(rt_scene_params), P(rt_prim), C.c_int32, C.c_int32, P(C.c_void_p)]),
+        "rt_scene_set_camera": (C.c_int, [C.c_void_p, P(rt_camera)]),
+        "rt_scene_set_traversal": (C.c_int, [C.c_void_p, C.c_int32]),
+        "rt_scene_get_info": (C.c_int, [C.c_void_p, P(rt_scene_info)]),
+        "rt_scene_destroy": (None, [C.c_void_p]),
+        "rt_render_tile": (C.c_int, [C.c_void_p] + [C.c_int32] * 5 + [C.c_uint64, C.c_uint64,
+                                     P(rt_color), P(C.c_uint32), P(C.c_uint32), P(C.c_uint64)]),
+        "rt_render_tile_1spp": (C.c_int, [C.c_void_p] + [C.c_int32] * 4 + [C.c_uint64, C.c_uint64, P(rt_color)]),
+        "rt_primary_ids": (C.c_int, [C.c_void_p] + [C.c_int32] * 4 + [P(C.c_int32)]),
+        "rt_render_device": (C.c_int, [C.c_void_p] + [C.c_int32] * 5 + [C.c_uint64, C.c_uint64] +
+                             [C.c_void_p] * 4 + [C.c_void_p]),
+        "rt_primary_ids_device": (C.c_int, [C.c_void_p] + [C.c_int32] * 4 + [C.c_void_p, C.c_void_p]),
+        "rt_last_kernel_ms": (C.c_int, [C.c_void_p, P(C.c_float)]),
+        "rt_render_frame_multi": (C.c_int, [P(rt_scene_params), P(rt_prim), C.c_int32, P(rt_camera), C.c_int32,
+                                            C.c_int32, C.c_uint64, P(rt_color), P(C.c_uint32), P(C.c_uint32),
+                                            P(C.c_uint64)]),
+        "rt_parse_scene": (C.c_int, [C.c_char_p, P(rt_scene_params), P(rt_prim), P(C.c_int32), P(rt_camera),
+                                     P(C.c_int32)]),
+        "rt_sample_output": (C.c_int32, [rt_color, C.c_uint32, C.c_uint32, rt_color, C.c_double, C.c_double]),
+        "rt_ref_bvh_export": (C.c_int, [P(rt_prim), C.c_int32, P(C.c_int32), P(C.c_double), P(C.c_int32),
+                                        P(C.c_int32)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(rc: int) -> None:
+    if rc != RT_OK:
+        buf = C.create_string_buffer(1024)
+        _lib.rt_last_error(buf, 1024)
+        raise RtError(f"rtcore error {rc}: {buf.value.decode(errors='replace')}")
+
+
+@dataclass
+class ParsedScene:
+    """SceneLoader.FromFile output in ABI form (Scene.cs fields + Primitives + Cameras)."""
+    params: rt_scene_params
+    prims: "C.Array[rt_prim]"
+    cameras: "C.Array[rt_camera]"
+
+    @property
+    def n_prims(self) -> int:
+        return len(self.prims)
+
+
+class SceneLoader:
+    """Mirror of RaytracerCore.SceneLoader (SceneLoader.cs:28-440) over rt_parse_scene."""
+
+    @staticmethod
+    def from_text(text: str) -> ParsedScene:
+        lib = load_library()
+        n_p, n_c = C.c_int32(0), C.c_int32(0)
+        params = rt_scene_params()
+        _check(lib.rt_parse_scene(text.encode(), C.byref(params), None, C.byref(n_p), None, C.byref(n_c)))
+        prims = (rt_prim * max(1, n_p.value))()
+        cams = (rt_camera * max(1, n_c.value))()
+        _check(lib.rt_parse_scene(text.encode(), C.byref(params), prims, C.byref(n_p), cams, C.byref(n_c)))
+        return ParsedScene(params, (rt_prim * n_p.value).from_buffer(prims), (rt_camera * n_c.value).from_buffer(cams))
+
+    @staticmethod
+    def from_file(path: str) -> ParsedScene:
+        with open(path, "r", encoding="utf-8") as f:
+            return SceneLoader.from_text(f.read())
+
+
+def ref_bvh_export(prims: Sequence[rt_prim]) -> Tuple[np.ndarray, np.ndarray, int, int]:
+    """The library's reference-BVH build (host code, no GPU): (leaf prim order, node boxes, nodes, depth)."""
+    lib = load_library()
+    n = len(prims)
+    arr = (rt_prim * max(1, n))(*prims)
+    order = np.zeros(max(1, n), np.int32)
+    boxes = np.zeros((max(1, 2 * n), 8), np.float64)
+    nodes, depth = C.c_int32(0), C.c_int32(0)
+    _check(lib.rt_ref_bvh_export(arr, n, order.ctypes.data_as(C.POINTER(C.c_int32)),
+                                 boxes.ctypes.data_as(C.POINTER(C.c_double)), C.byref(nodes), C.byref(depth)))
+    return order[:n], boxes[:nodes.value], nodes.value, depth.value
+
+
+def sample_output(sum_rgb: Tuple[float, float, float], samples: int, misses: int,
+                  background=(0.0, 0.0, 0.0), background_alpha: float = 0.0, exposure: float = 1.0) -> int:
+    """SampleSet.GetOutput (SampleSet.cs:61-113): ARGB int32."""
+    lib = load_library()
+    return lib.rt_sample_output(rt_color(*sum_rgb), samples, misses, rt_color(*background), background_alpha, exposure)
+
+
+def device_count() -> int:
+    return load_library().rt_device_count()
+
+
+class GpuRaytracer:
+    """One device scene: the drop-in for a `Raytracer` worker (Raytracer.cs:12-49, 294-330).
+
+    Tile buffers follow the C# DoubleColor[w, h] order: element (x, y) at x*h + y.
+    """
+
+    def __init__(self, scene: ParsedScene, camera_index: int = 0, device: int = 0,
+                 size: Optional[Tuple[int, int]] = None, traversal: int = RT_TRAVERSAL_AUTO):
+        lib = load_library()
+        self.lib = lib
+        self.params = rt_scene_params.from_buffer_copy(scene.params)
+        if size is not None:
+            self.params.width, self.params.height = int(size[0]), int(size[1])
+        self.width, self.height = self.params.width, self.params.height
+        self.handle = C.c_void_p()
+        n = scene.n_prims
+        prims = (rt_prim * max(1, n))(*scene.prims)
+        _check(lib.rt_scene_create(C.byref(self.params), prims, n, device, C.byref(self.handle)))
+        self.device = device
+        if len(scene.cameras) == 0:
+            raise RtError("scene has no camera")
+        self.camera = rt_camera.from_buffer_copy(scene.cameras[camera_index])
+        _check(lib.rt_scene_set_camera(self.handle, C.byref(self.camera)))
+        if traversal != RT_TRAVERSAL_AUTO:
+            self.set_traversal(traversal)
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.rt_scene_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_traversal(self, traversal: int) -> None:
+        _check(self.lib.rt_scene_set_traversal(self.handle, traversal))
+
+    def info(self) -> rt_scene_info:
+        inf = rt_scene_info()
+        _check(self.lib.rt_scene_get_info(self.handle, C.byref(inf)))
+        return inf
+
+    def primary_ids(self, x0: int = 0, y0: int = 0, w: Optional[int] = None, h: Optional[int] = None) -> np.ndarray:
+        """DebugRaycaster Primitives-mode IDs as an int32 array indexed [x, y]."""
+        w = self.width - x0 if w is None else w
+        h = self.height - y0 if h is None else h
+        ids = np.empty((w, h), np.int32)
+        _check(self.lib.rt_primary_ids(self.handle, x0, y0, w, h, ids.ctypes.data_as(C.POINTER(C.c_int32))))
+        return ids
+
+    def render_tile(self, x0: int, y0: int, w: int, h: int, spp: int, seed: int = 0, sample_base: int = 0):
+        """Accumulators (sum[w,h,3] f64, samples[w,h] u32, misses[w,h] u32, rays)."""
+        s = np.zeros((w, h, 3), np.float64)
+        n = np.zeros((w, h), np.uint32)
+        m = np.zeros((w, h), np.uint32)
+        rays = C.c_uint64(0)
+        _check(self.lib.rt_render_tile(self.handle, x0, y0, w, h, spp, seed, sample_base,
+                                       s.ctypes.data_as(C.POINTER(rt_color)),
+                                       n.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                       m.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(rays)))
+        return s, n, m, rays.value
+
+    def render_tile_1spp(self, x0: int, y0: int, w: int, h: int, seed: int = 0, sample_index: int = 0) -> np.ndarray:
+        """Raytracer.Render one pass: DoubleColor[w, h] with Placeholder (-1) for misses."""
+        out = np.empty((w, h, 3), np.float64)
+        _check(self.lib.rt_render_tile_1spp(self.handle, x0, y0, w, h, seed, sample_index,
+                                            out.ctypes.data_as(C.POINTER(rt_color))))
+        return out
+
+    def render_device(self, x0, y0, w, h, spp, seed, sample_base, d_sum, d_samples, d_misses, d_rays,
+                      stream: int = 0) -> None:
+        """Asynchronous device-resident render; d_* are device pointers (e.g. torch data_ptr())."""
+        _check(self.lib.rt_render_device(self.handle, x0, y0, w, h, spp, seed, sample_base,
+                                         C.c_void_p(d_sum), C.c_void_p(d_samples), C.c_void_p(d_misses),
+                                         C.c_void_p(d_rays), C.c_void_p(stream)))
+
+    def last_kernel_ms(self) -> float:
+        ms = C.c_float(0)
+        _check(self.lib.rt_last_kernel_ms(self.handle, C.byref(ms)))
+        return float(ms.value)
+
+
+def render_frame_multi(scene: ParsedScene, camera_index: int, n_gpus: int, spp: int, seed: int = 0,
+                       size: Optional[Tuple[int, int]] = None):
+    """rt_render_frame_multi: row-interleaved bands on n_gpus devices + RCCL gather."""
+    lib = load_library()
+    params = rt_scene_params.from_buffer_copy(scene.params)
+    if size is not None:
+        params.width, params.height = size
+    W, H = params.width, params.height
+    s = np.zeros((W, H, 3), np.float64)
+    n = np.zeros((W, H), np.uint32)
+    m = np.zeros((W, H), np.uint32)
+    rays = C.c_uint64(0)
+    prims = (rt_prim * max(1, scene.n_prims))(*scene.prims)
+    cam = rt_camera.from_buffer_copy(scene.cameras[camera_index])
+    _check(lib.rt_render_frame_multi(C.byref(params), prims, scene.n_prims, C.byref(cam), n_gpus, spp, seed,
+                                     s.ctypes.data_as(C.POINTER(rt_color)), n.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                     m.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(rays)))
+    return s, n, m, rays.value
+
+
+def scene_path(name: str) -> str:
+    """Path of a scene fixture shipped in tests/golden/scenes (bounce.txt, die.txt, ...)."""
+    return os.path.join(REPO_ROOT, "tests", "golden", "scenes", name)

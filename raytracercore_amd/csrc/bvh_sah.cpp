@@ -1,0 +1,234 @@
+// bvh_sah.cpp -- binned-SAH BVH2 for the fp32 path-tracing kernel.
+//
+// The kernel's own acceleration structure (the reference's agglomerative tree is kept only
+// for the exact primary-ID pass, bvh_ref.cpp).  Leaf boxes start from the reference's fp64
+// bounds (AABB.CreateFromBounded) rounded outward to fp32, so every primitive the fp64 query
+// could reach is still reached.  Nodes store both children's boxes (64 B per visit, one
+// cache line) and child references encode leaves inline (rt_internal.h NodeF).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "host_scene.h"
+
+namespace rtc {
+namespace {
+
+struct FBox {
+    float lo[3], hi[3];
+    void empty()
+    {
+        for (int i = 0; i < 3; i++) {
+            lo[i] = __builtin_huge_valf();
+            hi[i] = -__builtin_huge_valf();
+        }
+    }
+    void grow(const FBox& b)
+    {
+        for (int i = 0; i < 3; i++) {
+            lo[i] = std::min(lo[i], b.lo[i]);
+            hi[i] = std::max(hi[i], b.hi[i]);
+        }
+    }
+    float area() const
+    {
+        float d[3];
+        for (int i = 0; i < 3; i++) d[i] = std::max(0.0f, hi[i] - lo[i]);
+        return 2.0f * (d[0] * d[1] + d[1] * d[2] + d[2] * d[0]);
+    }
+};
+
+float round_down(double v)
+{
+    float f = (float)v;
+    if ((double)f > v) f = std::nextafter(f, -__builtin_huge_valf());
+    return f;
+}
+float round_up(double v)
+{
+    float f = (float)v;
+    if ((double)f < v) f = std::nextafter(f, __builtin_huge_valf());
+    return f;
+}
+
+struct BNode {
+    FBox box;
+    int left = -1, right = -1;
+    int first = 0, count = 0;
+};
+
+struct Ref {
+    int prim;
+    FBox box;
+    float c[3];
+};
+
+struct SahBuilder {
+    std::vector<Ref> refs;
+    std::vector<BNode> nodes;
+    int max_leaf;
+    int max_depth = 0;
+
+    int build(int first, int count, int depth)
+    {
+        max_depth = std::max(max_depth, depth);
+        BNode n;
+        n.box.empty();
+        FBox cb;
+        cb.empty();
+        for (int i = first; i < first + count; i++) {
+            n.box.grow(refs[i].box);
+            for (int k = 0; k < 3; k++) {
+                cb.lo[k] = std::min(cb.lo[k], refs[i].c[k]);
+                cb.hi[k] = std::max(cb.hi[k], refs[i].c[k]);
+            }
+        }
+        int me = (int)nodes.size();
+        nodes.push_back(n);
+        if (count <= max_leaf && count <= 8) {
+            nodes[me].first = first;
+            nodes[me].count = count;
+            return me;
+        }
+        // binned SAH over the centroid bounds
+        const int B = 32;
+        int best_axis = -1, best_split = -1;
+        float best_cost = __builtin_huge_valf();
+        for (int axis = 0; axis < 3; axis++) {
+            float ext = cb.hi[axis] - cb.lo[axis];
+            if (!(ext > 0)) continue;
+            FBox bb[B];
+            int bc[B];
+            for (int b = 0; b < B; b++) {
+                bb[b].empty();
+                bc[b] = 0;
+            }
+            float k = B / ext;
+            for (int i = first; i < first + count; i++) {
+                int b = std::min(B - 1, std::max(0, (int)((refs[i].c[axis] - cb.lo[axis]) * k)));
+                bb[b].grow(refs[i].box);
+                bc[b]++;
+            }
+            float rarea[B];
+            int rcount[B];
+            FBox acc;
+            acc.empty();
+            int cnt = 0;
+            for (int b = B - 1; b > 0; b--) {
+                acc.grow(bb[b]);
+                cnt += bc[b];
+                rarea[b] = acc.area();
+                rcount[b] = cnt;
+            }
+            acc.empty();
+            cnt = 0;
+            for (int b = 0; b < B - 1; b++) {
+                acc.grow(bb[b]);
+                cnt += bc[b];
+                if (cnt == 0 || rcount[b + 1] == 0) continue;
+                float cost = acc.area() * cnt + rarea[b + 1] * rcount[b + 1];
+                if (cost < best_cost) {
+                    best_cost = cost;
+                    best_axis = axis;
+                    best_split = b;
+                }
+            }
+        }
+        float leaf_cost = n.box.area() * count;
+        float split_cost = 0.125f * n.box.area() + best_cost; // traversal step ~1/8 of a primitive test
+        int mid;
+        if (best_axis < 0 || (count <= max_leaf && split_cost >= leaf_cost)) {
+            if (count <= max_leaf) {
+                nodes[me].first = first;
+                nodes[me].count = count;
+                return me;
+            }
+            // all centroids coincide (or no useful split): median split by index
+            mid = first + count / 2;
+        } else {
+            float ext = cb.hi[best_axis] - cb.lo[best_axis];
+            float k = B / ext;
+            auto it = std::partition(refs.begin() + first, refs.begin() + first + count, [&](const Ref& r) {
+                int b = std::min(B - 1, std::max(0, (int)((r.c[best_axis] - cb.lo[best_axis]) * k)));
+                return b <= best_split;
+            });
+            mid = (int)(it - refs.begin());
+            if (mid == first || mid == first + count) mid = first + count / 2;
+        }
+        int l = build(first, mid - first, depth + 1);
+        int r = build(mid, first + count - mid, depth + 1);
+        nodes[me].left = l;
+        nodes[me].right = r;
+        return me;
+    }
+};
+
+int leaf_ref(int first, int count) { return ~((first << 3) | (count - 1)); }
+
+} // namespace
+
+SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf)
+{
+    SahBvh out;
+    SahBuilder b;
+    b.max_leaf = std::max(1, std::min(8, max_leaf));
+    for (int i = 0; i < (int)prims.size(); i++) {
+        const HostPrim& p = prims[i];
+        if (p.kind == RT_PRIM_PLANE) continue;
+        Ref r;
+        r.prim = i;
+        const double lo[3] = {p.box.mn.x, p.box.mn.y, p.box.mn.z}, hi[3] = {p.box.mx.x, p.box.mx.y, p.box.mx.z};
+        for (int k = 0; k < 3; k++) {
+            // outward rounding plus a relative pad of 2^-20 against fp32 traversal rounding
+            double pad = (std::fabs(lo[k]) + std::fabs(hi[k])) * 9.5367431640625e-07 + 1e-30;
+            r.box.lo[k] = round_down(lo[k] - pad);
+            r.box.hi[k] = round_up(hi[k] + pad);
+            r.c[k] = 0.5f * (r.box.lo[k] + r.box.hi[k]);
+        }
+        b.refs.push_back(r);
+    }
+    if (b.refs.empty()) {
+        out.root = 0;
+        return out;
+    }
+    b.nodes.reserve(b.refs.size() * 2);
+    int root = b.build(0, (int)b.refs.size(), 0);
+    out.depth = b.max_depth;
+    for (const Ref& r : b.refs) out.order.push_back(r.prim);
+    // Emit internal nodes depth-first; the root gets index 0.
+    std::vector<int> remap(b.nodes.size(), -1);
+    std::vector<int> stack{root};
+    std::vector<int> internal;
+    while (!stack.empty()) {
+        int i = stack.back();
+        stack.pop_back();
+        if (b.nodes[i].left < 0) continue;
+        remap[i] = (int)internal.size();
+        internal.push_back(i);
+        stack.push_back(b.nodes[i].right);
+        stack.push_back(b.nodes[i].left);
+    }
+    auto ref_of = [&](int i) {
+        const BNode& n = b.nodes[i];
+        return n.left < 0 ? leaf_ref(n.first, n.count) : remap[i];
+    };
+    out.root = ref_of(root);
+    for (int i : internal) {
+        const BNode& n = b.nodes[i];
+        const BNode& l = b.nodes[n.left];
+        const BNode& r = b.nodes[n.right];
+        NodeF f;
+        int lr = ref_of(n.left), rr = ref_of(n.right);
+        float lw, rw;
+        std::memcpy(&lw, &lr, 4);
+        std::memcpy(&rw, &rr, 4);
+        f.lmin = make_float4(l.box.lo[0], l.box.lo[1], l.box.lo[2], lw);
+        f.lmax = make_float4(l.box.hi[0], l.box.hi[1], l.box.hi[2], 0.0f);
+        f.rmin = make_float4(r.box.lo[0], r.box.lo[1], r.box.lo[2], rw);
+        f.rmax = make_float4(r.box.hi[0], r.box.hi[1], r.box.hi[2], 0.0f);
+        out.nodes.push_back(f);
+    }
+    return out;
+}
+
+} // namespace rtc

@@ -1,0 +1,74 @@
+// host_scene.h -- host-side preparation of a scene for the MI355X kernels.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "rt_refmath.h"
+
+namespace rtc {
+
+// Axis-aligned box in the reference's fp64 representation (Acceleration/AABB.cs:44-64).
+struct Box {
+    Vec4d mn, mx, size, ctr;
+};
+Box box_make(Vec4d mn, Vec4d mx);
+Box box_combine(const Box& a, const Box& b); // AABB.Combine (AABB.cs:38-43)
+bool box_equals(const Box& a, const Box& b); // AABB.Equals (AABB.cs:232-241)
+double box_sa(const Box& b);                 // AABB.GetSurfaceArea (AABB.cs:204-207)
+
+// A primitive with the reference's derived fields (fp64).
+struct HostPrim {
+    int kind = 0;
+    uint32_t flags = 0; // rtc::F_* | kind
+    // triangle (Triangle.cs:22-29, Recalculate :54-66)
+    Vec4d v[3], vn[3], e01, e02, n;
+    // sphere (Sphere.cs:12-21)
+    Vec4d center;
+    double radius = 0, radius_sqr = 0;
+    double to_obj[16], to_world[16], to_normal[16];
+    // plane (Plane.cs:13-14)
+    Vec4d pn;
+    double pd = 0;
+    // material (raw backing fields)
+    rt_color emission, diffuse, specular, refraction;
+    double shininess = 100, ior = 0;
+    // bounds (AABB.CreateFromBounded, AABB.cs:22-36) and IBoundedObject center
+    Box box;
+    Vec4d center_pt;
+};
+
+std::vector<HostPrim> prepare_prims(const rt_prim* prims, int n);
+
+// The reference's agglomerative BVH, flattened depth-first (pre-order, left first).
+struct RefBvh {
+    std::vector<RefNode> nodes;
+    int depth = 0;
+};
+RefBvh build_ref_bvh(const std::vector<HostPrim>& prims);
+
+// Binned-SAH BVH2 for the fp32 path kernel (planes are excluded and tested separately).
+struct SahBvh {
+    std::vector<NodeF> nodes;
+    std::vector<int> order; // primitive IDs in leaf order
+    int root = 0;           // child reference of the root
+    int depth = 0;
+};
+SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf);
+
+// Camera.InitRender restated for both precisions.
+void camera_init(const rt_camera& cam, int width, int height, CameraD& d, CameraF& f);
+
+// Scene text loader (SceneLoader.cs:112-440).
+struct ParsedScene {
+    rt_scene_params params;
+    std::vector<rt_prim> prims;
+    std::vector<rt_camera> cameras;
+    rt_color background;
+    double background_alpha = 0;
+};
+bool parse_scene_text(const char* text, ParsedScene& out, std::string& err);
+
+// Thread-local error message used by rt_last_error().
+void set_error(const std::string& msg);
+
+} // namespace rtc

@@ -1,0 +1,589 @@
+// kernels_path.hip -- the persistent fp32 path-tracing kernel for gfx950.
+//
+// One launch renders `spp` samples for every pixel of a tile.  Work items are
+// (sample chunk, pixel) pairs dealt out by a wave-aggregated atomic; each lane owns one item
+// at a time and regenerates a new camera path the iteration after its previous path ends,
+// so every loop iteration issues exactly one closest-hit query (Scene.RayTrace) per live
+// lane.  Per item the lane accumulates its chunk's samples in registers and writes one
+// 16-byte partial; a second kernel folds the partials into fp64 accumulators in a fixed
+// order, so results do not depend on scheduling.
+//
+// Per path this restates Raytracer.GetCameraRay + GetColor (Raytracer.cs:51-287):
+//   camera jitter and depth of field, the bounce loop with RandomShine (rough normal),
+//   Fresnel / total internal reflection, the luminance-weighted transmit / specular /
+//   diffuse / emission choice, tint *= colour * max(totalLum, 1), and the miss rules
+//   (primary miss -> Placeholder/miss, secondary miss -> AmbientRGB untinted).
+// The closest-hit query restates Scene.RayTrace semantics (Scene.cs:65-120, Primitive.cs:46-75)
+// in fp32: strict-closest hit, Invert flipping Inside only, one-sided culling, and
+// Util.RayHitMatches' self-hit rejection (Util.cs:179-192) restated as: a flat primitive
+// is never re-hit by the ray leaving it; a sphere re-hit keeps only the far root when the
+// ray heads into it (DESIGN.md §Self-hit rule).
+#include "../../include/rtcore_rng.h"
+#include "rt_kernels.h"
+
+namespace rtc {
+namespace {
+
+struct V3 {
+    float x, y, z;
+};
+__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 xyz(float4 a) { return V3{a.x, a.y, a.z}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ V3 operator*(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ V3 operator*(V3 a, V3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ V3 operator-(V3 a) { return {-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ float dot(V3 a, V3 b) { return fmaf(a.x, b.x, fmaf(a.y, b.y, a.z * b.z)); }
+__device__ __forceinline__ V3 cross(V3 a, V3 b)
+{
+    return {fmaf(a.y, b.z, -a.z * b.y), fmaf(a.z, b.x, -a.x * b.z), fmaf(a.x, b.y, -a.y * b.x)};
+}
+__device__ __forceinline__ V3 madd(V3 a, float s, V3 c) { return {fmaf(a.x, s, c.x), fmaf(a.y, s, c.y), fmaf(a.z, s, c.z)}; }
+__device__ __forceinline__ V3 normalize(V3 a)
+{
+    float r = __builtin_amdgcn_rsqf(dot(a, a));
+    return a * r;
+}
+__device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ V3 xf_point(const float4* m, V3 p)
+{
+    return {fmaf(m[0].x, p.x, fmaf(m[0].y, p.y, fmaf(m[0].z, p.z, m[0].w))),
+            fmaf(m[1].x, p.x, fmaf(m[1].y, p.y, fmaf(m[1].z, p.z, m[1].w))),
+            fmaf(m[2].x, p.x, fmaf(m[2].y, p.y, fmaf(m[2].z, p.z, m[2].w)))};
+}
+__device__ __forceinline__ V3 xf_dir(const float4* m, V3 p)
+{
+    return {fmaf(m[0].x, p.x, fmaf(m[0].y, p.y, m[0].z * p.z)), fmaf(m[1].x, p.x, fmaf(m[1].y, p.y, m[1].z * p.z)),
+            fmaf(m[2].x, p.x, fmaf(m[2].y, p.y, m[2].z * p.z))};
+}
+
+struct Best {
+    float t;    // world distance (Hit.Distance)
+    int slot;   // index into the primitive array of the traversal mode, -1 = none
+    float u, v; // triangle barycentrics | sphere: object-space ray parameter in u
+    int gin;    // geometric inside before Invert (selects the flipped normal)
+};
+
+__device__ __forceinline__ void test_tri(const PrimF& P, int slot, V3 o, V3 d, int prev, Best& b)
+{
+    const int id = __float_as_int(P.a.w);
+    if (id == prev) return; // a flat primitive cannot be re-hit after leaving it
+    const uint32_t fl = __float_as_uint(P.b.w);
+    const V3 off = o - xyz(P.a);
+    const V3 e1 = xyz(P.b), e2 = xyz(P.c);
+    const V3 s1 = cross(off, e1);
+    const V3 s2 = cross(d, e2);
+    const float inv = rcp(dot(e1, s2));
+    const float t = dot(e2, s1) * inv;
+    if (!(t >= 0.0f && t < b.t)) return;
+    const float u = dot(off, s2) * inv, v = dot(d, s1) * inv;
+    const bool rej = (u < 0.0f) | (v < 0.0f) | ((fl & F_MIRROR) ? ((u > 1.0f) | (v > 1.0f)) : (u + v > 1.0f));
+    if (rej) return;
+    const int gin = inv < 0.0f;
+    const bool ins = gin ^ ((fl & F_INVERT) != 0);
+    if (ins && !(fl & F_TWOSIDED)) return;
+    b = Best{t, slot, u, v, gin};
+}
+
+__device__ __forceinline__ void test_sph(const PrimF& P, int slot, V3 o, V3 d, int prev, const XformF* xf, Best& b)
+{
+    const int id = __float_as_int(P.a.w);
+    const uint32_t fl = __float_as_uint(P.b.w);
+    V3 oo = o, dd = d;
+    float k = 1.0f; // object-space ray parameter -> world distance
+    if (fl & F_TRANSFORMED) {
+        const XformF& X = xf[__float_as_int(P.b.z)];
+        oo = xf_point(X.to_world, o);
+        V3 dl = xf_dir(X.to_world, d);
+        float il = __builtin_amdgcn_rsqf(dot(dl, dl));
+        dd = dl * il;
+        k = il; // |to_obj * dd| = 1 / |to_world * d|
+    }
+    const V3 oc = oo - xyz(P.a);
+    const float bb = dot(oc, dd);
+    float tn = -1.0f, tf;
+    if (id == prev) {
+        // the root at the bounce point is the skipped self-hit; the other root is -2 (oc.dd)
+        if (!(bb < 0.0f)) return;
+        tf = -2.0f * bb;
+    } else {
+        const V3 l = madd(dd, -bb, oc);
+        const float disc = P.b.y - dot(l, l);
+        if (!(disc >= 0.0f)) return;
+        const float sq = sqrtf(disc);
+        tn = -bb - sq;
+        tf = -bb + sq;
+        if (!(tf >= 0.0f)) return;
+    }
+    const bool inv = (fl & F_INVERT) != 0, two = (fl & F_TWOSIDED) != 0;
+    if (tn >= 0.0f && (two || !inv)) { // close hit: Inside = false (^ Invert)
+        const float tw = tn * k;
+        if (tw < b.t) b = Best{tw, slot, tn, 0.0f, 0};
+        return;
+    }
+    if (two || inv) { // far hit: Inside = true (^ Invert)
+        const float tw = tf * k;
+        if (tw < b.t) b = Best{tw, slot, tf, 0.0f, 1};
+    }
+}
+
+__device__ __forceinline__ void test_plane(const PrimF& P, int slot, V3 o, V3 d, int prev, Best& b)
+{
+    const int id = __float_as_int(P.a.w);
+    if (id == prev) return;
+    const uint32_t fl = __float_as_uint(P.b.w);
+    const V3 n = xyz(P.a);
+    const float pd = P.b.x;
+    const float rd = dot(o, n), den = dot(d, n);
+    float dist;
+    int gin;
+    if (den == 0.0f) {
+        // Plane.DoRayTrace's NearlyEqual branch (Plane.cs:41-45, Util.cs:41-51)
+        if (!(pd == rd || fmaxf(pd, rd) < 0.0f)) return;
+        dist = 0.0f;
+        gin = 1;
+    } else {
+        const float t = (pd - rd) / den;
+        if (!(t >= -1e-24f)) return;
+        dist = fabsf(t);
+        gin = dot(n, d) > 0.0f;
+    }
+    const bool ins = gin ^ ((fl & F_INVERT) != 0);
+    if (ins && !(fl & F_TWOSIDED)) return;
+    if (dist < b.t) b = Best{dist, slot, dist, 0.0f, gin};
+}
+
+// Closest hit over every primitive; the loop index is wave-uniform, so the primitive
+// records stream through the scalar data cache.
+__device__ __forceinline__ void trace_brute(const DevScene& s, V3 o, V3 d, int prev, Best& b, unsigned long long* st)
+{
+    const PrimF* __restrict__ P = s.prims_bf;
+    int i = 0;
+    for (; i < s.n_tri; i++) test_tri(P[i], i, o, d, prev, b);
+    for (; i < s.n_tri + s.n_sph; i++) test_sph(P[i], i, o, d, prev, s.xf, b);
+}
+
+
+__device__ __forceinline__ bool slab(float4 lo, float4 hi, V3 oi, V3 id, float tmax, float& tnear)
+{
+    // t = box * (1/d) - o * (1/d); NaN from 0*inf is ignored by fminf/fmaxf (conservative)
+    const float tx0 = fmaf(lo.x, id.x, -oi.x), tx1 = fmaf(hi.x, id.x, -oi.x);
+    const float ty0 = fmaf(lo.y, id.y, -oi.y), ty1 = fmaf(hi.y, id.y, -oi.y);
+    const float tz0 = fmaf(lo.z, id.z, -oi.z), tz1 = fmaf(hi.z, id.z, -oi.z);
+    const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    const float tmx = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    tnear = tmin;
+    return tmin <= tmx * 1.00000024f;
+}
+
+template <int STACK>
+__device__ __forceinline__ void trace_bvh(const DevScene& s, V3 o, V3 d, int prev, Best& b, int* stk,
+                                          unsigned long long* st)
+{
+    const V3 id = v3(rcp(d.x), rcp(d.y), rcp(d.z));
+    const V3 oi = o * id;
+    int ref = s.root;
+    int sp = 0;
+    while (true) {
+        if (ref >= 0) {
+            const NodeF n = s.nodes[ref];
+            float tl, tr;
+            const bool hl = slab(n.lmin, n.lmax, oi, id, b.t, tl);
+            const bool hr = slab(n.rmin, n.rmax, oi, id, b.t, tr);
+            const int cl = __float_as_int(n.lmin.w), cr = __float_as_int(n.rmin.w);
+            if (hl && hr) {
+                const bool lf = tl <= tr;
+                if (sp < STACK) stk[(sp++) * 256] = lf ? cr : cl; // host guarantees depth < STACK
+                ref = lf ? cl : cr;
+                continue;
+            }
+            if (hl) { ref = cl; continue; }
+            if (hr) { ref = cr; continue; }
+        } else {
+            const int code = ~ref;
+            const int first = code >> 3, cnt = (code & 7) + 1;
+            for (int k = first; k < first + cnt; k++) {
+                const PrimF P = s.prims_bvh[k];
+                if ((__float_as_uint(P.b.w) & KIND_MASK) == RT_PRIM_TRIANGLE)
+                    test_tri(P, k, o, d, prev, b);
+                else
+                    test_sph(P, k, o, d, prev, s.xf, b);
+            }
+        }
+        if (sp == 0) break;
+        ref = stk[(--sp) * 256];
+    }
+}
+
+struct Sample {
+    V3 o, d, tint;
+    int bounce;
+    int prev;
+    rt_rng rng;
+};
+
+__device__ __forceinline__ float next_u(rt_rng& r) { return rt_rng_next_float(&r); }
+
+// Vec4D.CreateHorizon(pole, z, theta) (Vec4D.cs:52-58) as the equivalent Rodrigues form:
+// pole*z + (c*cos(theta) + (pole x c)*sin(theta)) * s, c = normalize(pole x z^) or x^.
+__device__ __forceinline__ V3 horizon(V3 pole, float z, float s, float turn)
+{
+    V3 c = v3(pole.y, -pole.x, 0.0f);
+    const float cl = c.x * c.x + c.y * c.y;
+    c = (cl == 0.0f) ? v3(1.0f, 0.0f, 0.0f) : c * __builtin_amdgcn_rsqf(cl);
+    const V3 bn = cross(pole, c);
+    const float cs = __builtin_amdgcn_cosf(turn), sn = __builtin_amdgcn_sinf(turn); // argument in turns
+    const V3 h = madd(c, cs, bn * sn);
+    return madd(h, s, pole * z);
+}
+
+__device__ __forceinline__ void camera_ray(const CameraF& c, float x, float y, V3& o, V3& d)
+{
+    if (c.kind == RT_CAMERA_FRUSTUM) {
+        const float ox = c.tan_x * ((x - c.w2) / c.w2);
+        const float oy = c.tan_y * ((y - c.h2) / c.h2);
+        d = normalize(madd(xyz(c.up), oy, madd(xyz(c.side), ox, xyz(c.look))));
+        o = xyz(c.position);
+    } else {
+        o = madd(xyz(c.up), (y - c.h2) * c.v_mult, madd(xyz(c.side), (x - c.w2) * c.h_mult, xyz(c.position)));
+        d = normalize(xyz(c.look));
+    }
+    o = madd(d, c.image_plane, o);
+}
+
+// Raytracer.GetCameraRay (Raytracer.cs:262-282)
+__device__ __forceinline__ void start_sample(const CameraF& cam, int x, int y, Sample& S)
+{
+    const float sx = (float)x + next_u(S.rng);
+    const float sy = (float)y + next_u(S.rng);
+    camera_ray(cam, sx, sy, S.o, S.d);
+    if (cam.dof != 0.0f) {
+        const V3 focus = madd(S.d, cam.focal_length - cam.image_plane, S.o);
+        const float dist = sqrtf(next_u(S.rng)) * cam.dof;
+        const float turn = next_u(S.rng);
+        const float ox = __builtin_amdgcn_cosf(turn) * dist, oy = __builtin_amdgcn_sinf(turn) * dist;
+        V3 o2, d2;
+        camera_ray(cam, sx + ox, sy + oy, o2, d2);
+        S.o = o2;
+        S.d = normalize(focus - o2);
+    }
+    S.tint = v3(1.0f, 1.0f, 1.0f);
+    S.bounce = 0;
+    S.prev = -1;
+}
+
+// One bounce of Raytracer.GetColor after the closest-hit query.  Returns 0 to continue the
+// path, 1 if the sample ended with colour `col`, 2 if it ended as a miss (Placeholder).
+__device__ __forceinline__ int shade(const DevScene& s, const PrimF* prims, const Best& b, Sample& S, V3& col)
+{
+    if (b.slot < 0) {
+        if (S.bounce == 0 || s.ambient_miss) return 2;
+        col = v3(s.ambient.x, s.ambient.y, s.ambient.z);
+        return 1;
+    }
+    const PrimF P = prims[b.slot];
+    const uint32_t fl = __float_as_uint(P.b.w);
+    const int id = __float_as_int(P.a.w);
+    const MatF& M = s.mats[id];
+    const uint32_t kind = fl & KIND_MASK;
+    const V3 emis = xyz(M.emission);
+    if (s.debug_geom) { // Raytracer.cs:93-98
+        col = xyz(M.specular) + xyz(M.diffuse) + emis;
+        return 1;
+    }
+    if (S.bounce >= s.recursion) {
+        col = S.tint * emis;
+        return 1;
+    }
+    // hit position and normal facing the incoming ray
+    V3 pos, nrm;
+    if (kind == RT_PRIM_TRIANGLE) {
+        pos = madd(xyz(P.b), b.u, madd(xyz(P.c), b.v, xyz(P.a)));
+        if (fl & F_HASNORMALS) { // Triangle.GetNormal quirk: Normal is never set -> NaN when inside
+            const float4* vn = s.vnormals + 3 * id;
+            nrm = normalize(madd(xyz(vn[2]), b.u + b.v, madd(xyz(vn[1]), b.v, xyz(vn[0]) * b.u)));
+            if (b.gin) nrm = v3(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
+        } else {
+            nrm = b.gin ? -xyz(P.d) : xyz(P.d);
+        }
+    } else if (kind == RT_PRIM_SPHERE) {
+        V3 oo = S.o, dd = S.d;
+        const bool tr = (fl & F_TRANSFORMED) != 0;
+        const XformF* X = tr ? &s.xf[__float_as_int(P.b.z)] : nullptr;
+        if (tr) {
+            oo = xf_point(X->to_world, S.o);
+            dd = normalize(xf_dir(X->to_world, S.d));
+        }
+        const V3 op = madd(dd, b.u, oo);
+        V3 n = (op - xyz(P.a)) * rcp(P.b.x);
+        if (tr) {
+            pos = xf_point(X->to_obj, op);
+            n = normalize(xf_dir(X->to_normal, n));
+        } else {
+            pos = op;
+        }
+        nrm = b.gin ? -n : n;
+    } else {
+        pos = madd(S.d, b.u, S.o);
+        nrm = b.gin ? -xyz(P.a) : xyz(P.a);
+    }
+    const bool inside = b.gin ^ ((fl & F_INVERT) != 0);
+
+    // RandomShine (Raytracer.cs:51-56): z = U^(1/shininess), theta = U * 2pi
+    const float shin = M.shininess;
+    float z = 1.0f, sz = 0.0f;
+    if (!(__builtin_isinf(shin) && shin > 0.0f)) {
+        const float a = __builtin_amdgcn_logf(next_u(S.rng)) / shin; // log2
+        z = __builtin_amdgcn_exp2f(a);
+        sz = sqrtf(-expm1f(2.0f * a * 0.69314718055994531f)); // sqrt(1 - z^2) without cancellation
+    }
+    const V3 rough = horizon(nrm, z, sz, next_u(S.rng));
+
+    const float diff_lum = M.diffuse.w, emis_lum = M.emission.w;
+    float spec_lum = M.specular.w, refr_lum = M.refraction.w;
+    const float cs = -dot(rough, S.d);
+    float cos_out = 0.0f, ior_ratio = 0.0f;
+    if (((refr_lum > 0.0f) | (spec_lum > 0.0f)) && M.ior != 0.0f && cs >= 0.0f) { // Raytracer.cs:120-161
+        const float ior_in = inside ? M.ior : s.air_ior;
+        const float ior_out = inside ? s.air_ior : M.ior;
+        ior_ratio = ior_in / ior_out;
+        const float sin_out = ior_ratio * sqrtf(1.0f - cs * cs);
+        if (sin_out >= 1.0f) {
+            refr_lum = 0.0f;
+        } else {
+            cos_out = sqrtf(1.0f - sin_out * sin_out);
+            const float rs = (ior_out * cs - ior_in * cos_out) / (ior_out * cs + ior_in * cos_out);
+            const float rp = (ior_in * cs - ior_out * cos_out) / (ior_in * cs + ior_out * cos_out);
+            const float ratio = (rs * rs + rp * rp) * 0.5f;
+            spec_lum *= ratio;
+            refr_lum *= 1.0f - ratio;
+        }
+    } else {
+        refr_lum = 0.0f;
+    }
+    const float total = diff_lum + spec_lum + refr_lum + emis_lum;
+    if (total <= 0.0f) {
+        col = S.tint * emis;
+        return 1;
+    }
+    float ray_rand = next_u(S.rng) * total;
+    V3 out_dir;
+    V3 new_tint;
+    if (refr_lum != 0.0f && (ray_rand -= refr_lum) <= 0.0f) { // transmission
+        out_dir = madd(madd(rough, cs, S.d), ior_ratio, rough * (-cos_out));
+        new_tint = inside ? v3(1.0f, 1.0f, 1.0f) : xyz(M.refraction);
+    } else if (spec_lum != 0.0f && (ray_rand -= spec_lum) <= 0.0f) { // specular
+        out_dir = madd(rough, 2.0f * cs, S.d);
+        if (!(dot(out_dir, nrm) > 0.0f)) {
+            col = S.tint * emis;
+            return 1;
+        }
+        new_tint = xyz(M.specular);
+    } else if (diff_lum != 0.0f && (ray_rand -= diff_lum) <= 0.0f) { // diffuse
+        const float dz = 2.0f * acosf(next_u(S.rng)) * 0.31830988618379067f;
+        const float ds = sqrtf(fmaxf(0.0f, 1.0f - dz * dz));
+        out_dir = horizon(nrm, dz, ds, next_u(S.rng));
+        new_tint = xyz(M.diffuse);
+    } else { // emission
+        col = S.tint * emis;
+        return 1;
+    }
+    S.o = pos;
+    S.d = normalize(out_dir);
+    S.prev = id;
+    S.tint = S.tint * (new_tint * fmaxf(total, 1.0f));
+    S.bounce++;
+    return 0;
+}
+
+// TRAV: RT_TRAVERSAL_BRUTE, or RT_TRAVERSAL_BVH with an LDS stack of STACK entries per lane.
+template <int TRAV, int STACK, bool STATS>
+__global__ void __launch_bounds__(256) path_kernel(DevScene s, CameraF cam, PathParams p)
+{
+    __shared__ int stack_mem[TRAV == RT_TRAVERSAL_BVH ? STACK * 256 : 1];
+    int* stk = stack_mem + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const unsigned total = (unsigned)p.n_chunks * (unsigned)p.n_pad;
+    const PrimF* prims = TRAV == RT_TRAVERSAL_BVH ? s.prims_bvh : s.prims_bf;
+
+    bool active = true, item_open = false, live = false;
+    unsigned item = 0;
+    int px = 0, py = 0, s_next = 0, s_end = 0;
+    float ar = 0.0f, ag = 0.0f, ab = 0.0f;
+    unsigned n_s = 0, n_m = 0, rays = 0;
+    Sample S;
+    S.prev = -1;
+    S.bounce = 0;
+
+    while (true) {
+        const bool need = active && !live && (!item_open || s_next >= s_end);
+        if (need && item_open) {
+            p.partial[item] = make_float4(ar, ag, ab, __uint_as_float(n_s | (n_m << 16)));
+            item_open = false;
+        }
+        const unsigned long long m = __ballot(need);
+        if (m) {
+            const int leader = __ffsll((long long)m) - 1;
+            unsigned base = 0;
+            if (lane == leader) base = atomicAdd(p.counter, (unsigned)__popcll(m));
+            base = __shfl(base, leader);
+            if (need) {
+                item = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+                if (item >= total) {
+                    active = false;
+                } else {
+                    const int c = (int)(item / (unsigned)p.n_pad);
+                    const int q = (int)(item - (unsigned)c * (unsigned)p.n_pad);
+                    const int blk = q >> 6, wi = q & 63;
+                    px = (blk % p.blocks_x) * 8 + (wi & 7);
+                    py = (blk / p.blocks_x) * 8 + (wi >> 3);
+                    if (px < p.w && py < p.h) {
+                        item_open = true;
+                        s_next = c * p.chunk;
+                        s_end = min(p.spp, s_next + p.chunk);
+                        ar = ag = ab = 0.0f;
+                        n_s = n_m = 0;
+                    }
+                }
+            }
+        }
+        if (!__any(active)) break;
+        if (active && item_open && !live && s_next < s_end) {
+            const int fx = p.x0 + px;
+            const int fy = p.band > 0 ? p.y0 + ((py / p.band) * p.band_stride + p.band_offset) * p.band + py % p.band
+                                      : p.y0 + py;
+            S.rng = rt_rng_init(p.seed, (unsigned long long)fy * (unsigned long long)s.width + (unsigned long long)fx,
+                                p.sample_base + (unsigned long long)s_next);
+            start_sample(cam, fx, fy, S);
+            live = true;
+        }
+        if (live) {
+            Best b{__builtin_huge_valf(), -1, 0.0f, 0.0f, 0};
+            if (TRAV == RT_TRAVERSAL_BVH) {
+                trace_bvh<STACK>(s, S.o, S.d, S.prev, b, stk, STATS ? p.stats : nullptr);
+            } else {
+                trace_brute(s, S.o, S.d, S.prev, b, STATS ? p.stats : nullptr);
+            }
+            for (int i = 0; i < s.n_pln; i++) test_plane(s.prims_bf[s.n_tri + s.n_sph + i], s.n_tri + s.n_sph + i, S.o,
+                                                       S.d, S.prev, b);
+            rays++;
+            V3 col;
+            // planes live in the brute-force array in both modes
+            const bool plane_hit = b.slot >= s.n_tri + s.n_sph && TRAV == RT_TRAVERSAL_BVH;
+            const int r = plane_hit ? shade(s, s.prims_bf, b, S, col) : shade(s, prims, b, S, col);
+            if (r != 0) {
+                if (r == 1) {
+                    ar += col.x;
+                    ag += col.y;
+                    ab += col.z;
+                    n_s++;
+                } else {
+                    n_m++;
+                }
+                s_next++;
+                live = false;
+            }
+        }
+    }
+    // one 64-bit add per wave for the ray count
+    unsigned long long wr = rays;
+    for (int off = 32; off > 0; off >>= 1) wr += __shfl_down(wr, off);
+    if (lane == 0) atomicAdd(p.rays, wr);
+}
+
+__global__ void accumulate_kernel(PathParams p, double* sum, uint32_t* samples, uint32_t* misses)
+{
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
+    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= p.w || y >= p.h) return;
+    const int q = ((y >> 3) * p.blocks_x + (x >> 3)) * 64 + (y & 7) * 8 + (x & 7);
+    const size_t npix = (size_t)p.w * p.h, i = (size_t)y * p.w + x;
+    double r = sum[i], g = sum[npix + i], bl = sum[2 * npix + i];
+    uint32_t ns = 0, nm = 0;
+    for (int c = 0; c < p.n_chunks; c++) {
+        const float4 v = p.partial[(size_t)c * p.n_pad + q];
+        r += v.x;
+        g += v.y;
+        bl += v.z;
+        const uint32_t k = __float_as_uint(v.w);
+        ns += k & 0xFFFFu;
+        nm += k >> 16;
+    }
+    sum[i] = r;
+    sum[npix + i] = g;
+    sum[2 * npix + i] = bl;
+    samples[i] += ns;
+    misses[i] += nm;
+}
+
+__global__ void colors_1spp_kernel(PathParams p, double* out)
+{
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
+    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= p.w || y >= p.h) return;
+    const int q = ((y >> 3) * p.blocks_x + (x >> 3)) * 64 + (y & 7) * 8 + (x & 7);
+    const float4 v = p.partial[q];
+    const bool miss = (__float_as_uint(v.w) & 0xFFFFu) == 0;
+    const size_t o = ((size_t)x * p.h + y) * 3; // DoubleColor[w, h]: x*h + y
+    out[o + 0] = miss ? -1.0 : (double)v.x;
+    out[o + 1] = miss ? -1.0 : (double)v.y;
+    out[o + 2] = miss ? -1.0 : (double)v.z;
+}
+
+using PathKernel = void (*)(DevScene, CameraF, PathParams);
+
+// traversal: 0 brute force, 1 BVH with a 24-entry stack, 2 BVH with a 48-entry stack
+PathKernel pick(int variant, bool stats)
+{
+    switch (variant) {
+    case 1: return stats ? path_kernel<RT_TRAVERSAL_BVH, 24, true> : path_kernel<RT_TRAVERSAL_BVH, 24, false>;
+    case 2: return stats ? path_kernel<RT_TRAVERSAL_BVH, 48, true> : path_kernel<RT_TRAVERSAL_BVH, 48, false>;
+    default: return stats ? path_kernel<RT_TRAVERSAL_BRUTE, 1, true> : path_kernel<RT_TRAVERSAL_BRUTE, 1, false>;
+    }
+}
+
+} // namespace
+
+int path_variant(int traversal, int bvh_depth)
+{
+    if (traversal != RT_TRAVERSAL_BVH) return 0;
+    return bvh_depth < 24 ? 1 : 2;
+}
+
+int path_blocks_per_cu(int variant, bool stats)
+{
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(pick(variant, stats)), 256, 0) !=
+            hipSuccess ||
+        n < 1)
+        n = 1;
+    return n;
+}
+
+hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& p, int variant, int grid_blocks,
+                       hipStream_t stream, bool stats)
+{
+    DevScene sa = s;
+    CameraF ca = cam;
+    PathParams pa = p;
+    void* args[] = {&sa, &ca, &pa};
+    return hipLaunchKernel(reinterpret_cast<const void*>(pick(variant, stats)), dim3(grid_blocks), dim3(256), args, 0,
+                           stream);
+}
+
+hipError_t launch_accumulate(const PathParams& p, double* d_sum, uint32_t* d_samples, uint32_t* d_misses, hipStream_t stream)
+{
+    dim3 grid((p.w + 15) / 16, (p.h + 15) / 16);
+    hipLaunchKernelGGL(accumulate_kernel, grid, dim3(256), 0, stream, p, d_sum, d_samples, d_misses);
+    return hipGetLastError();
+}
+
+hipError_t launch_colors_1spp(const PathParams& p, double* d_out, hipStream_t stream)
+{
+    dim3 grid((p.w + 15) / 16, (p.h + 15) / 16);
+    hipLaunchKernelGGL(colors_1spp_kernel, grid, dim3(256), 0, stream, p, d_out);
+    return hipGetLastError();
+}
+
+} // namespace rtc

@@ -1,0 +1,127 @@
+// rt_internal.h -- internal data layout of the MI355X path-tracing core.
+//
+// Two device representations of one scene are built on the host:
+//   * the EXACT fp64 set (PrimD + RefNode): the reference's own agglomerative BVH
+//     (Acceleration/BVH.cs:193-236) flattened in depth-first order, used by the
+//     DebugRaycaster-equivalent primary-ID kernel that must match the reference's
+//     closest-hit query bit for bit (Scene.cs:65-111);
+//   * the FAST fp32 set (PrimF + NodeF): a binned-SAH BVH2 whose nodes carry both child
+//     boxes (one 64-B line per visit), used by the persistent path-tracing kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rtcore.h"
+
+namespace rtc {
+
+// ---- flags packed into PrimF / PrimD -------------------------------------------------
+enum : uint32_t {
+    KIND_MASK = 3u,     // rt_prim_kind in bits 0-1
+    F_MIRROR = 1u << 2,
+    F_TWOSIDED = 1u << 3,
+    F_INVERT = 1u << 4,
+    F_HASNORMALS = 1u << 5,
+    F_TRANSFORMED = 1u << 6,
+};
+
+// ---- exact fp64 scene (primary-ID pass) -----------------------------------------------
+struct alignas(16) Vec4d {
+    double x, y, z, w;
+};
+
+struct alignas(16) PrimD {      // 256 B
+    Vec4d a, b, c, d;           // tri: v0, e01, e02, N | sphere: center, (r, r^2) | plane: N, (dist)
+    Vec4d vn[3];                // triangle vertex normals (HasNormals)
+    uint32_t flags;
+    int32_t xf;                 // index into XformD for transformed spheres, else -1
+    int32_t pad[6];
+};
+
+struct alignas(16) XformD {     // MatrixToWorld, MatrixToObject, MatrixToNormal (row-major)
+    double to_world[16];
+    double to_obj[16];
+    double to_normal[16];
+};
+
+struct alignas(16) RefNode {    // 80 B, depth-first pre-order; left child = this + 1
+    Vec4d mn, mx;
+    int32_t right;              // index of the right child (internal) or -1
+    int32_t prim;               // leaf: primitive index, internal: -1
+    int32_t skip;               // BVH<T>.SkipVolume (BVH.cs:44-48)
+    int32_t pad;
+};
+
+// ---- fast fp32 scene (path tracing) --------------------------------------------------
+struct alignas(16) PrimF {      // 64 B
+    float4 a; // tri: v0.xyz, id | sphere: c.xyz, id | plane: N.xyz, id
+    float4 b; // tri: e01.xyz, flags | sphere: (r, r^2, xf, flags) | plane: (dist, 0, 0, flags)
+    float4 c; // tri: e02.xyz, 0
+    float4 d; // tri: N.xyz, 0
+};
+
+struct alignas(16) XformF {     // rows 0-2 of each 4x4 (last row is 0 0 0 1)
+    float4 to_world[3];
+    float4 to_obj[3];
+    float4 to_normal[3];
+};
+
+struct alignas(16) MatF {       // per primitive ID, 80 B
+    float4 emission;            // rgb, luminance
+    float4 diffuse;             // rgb, luminance
+    float4 specular;            // rgb (Shininess<=0 -> black), luminance
+    float4 refraction;          // rgb (Shininess<=0 -> black), luminance
+    float shininess;            // may be +inf
+    float ior;                  // RefractiveIndex
+    uint32_t flags;
+    float pad;
+};
+
+// Child reference in a NodeF: >= 0 internal node index, < 0 leaf = ~(first << 3 | (count-1)).
+struct alignas(16) NodeF {      // 64 B: both children's boxes
+    float4 lmin; // xyz, w = bitcast int left child
+    float4 lmax; // xyz, w unused
+    float4 rmin; // xyz, w = bitcast int right child
+    float4 rmax;
+};
+
+struct CameraF {                // post-InitRender state in fp32 (path kernel)
+    float4 position, look, side, up;
+    float w2, h2, tan_x, tan_y, h_mult, v_mult, image_plane, dof, focal_length;
+    int32_t kind;
+};
+
+struct CameraD {                // post-InitRender state in fp64 (exact kernel)
+    Vec4d position, look, side, up;
+    double w2, h2, tan_x, tan_y, h_mult, v_mult, image_plane, dof, focal_length;
+    int32_t kind;
+    int32_t pad;
+};
+
+// Everything a kernel needs, passed by value.
+struct DevScene {
+    // fast set
+    const PrimF* prims_bf;      // brute-force order: triangles | spheres | planes
+    int32_t n_tri, n_sph, n_pln;
+    const PrimF* prims_bvh;     // BVH leaf order (planes excluded: always brute force)
+    const NodeF* nodes;
+    int32_t n_nodes;
+    int32_t root;               // child reference of the root (may be a leaf)
+    const XformF* xf;
+    const MatF* mats;
+    const float4* vnormals;     // 3 per primitive ID (HasNormals triangles)
+    // exact set
+    const PrimD* prims_d;
+    const XformD* xf_d;
+    const RefNode* ref_nodes;
+    int32_t n_ref_nodes;
+    // scene fields
+    int32_t width, height;
+    int32_t recursion;
+    int32_t debug_geom;
+    float air_ior;
+    float3 ambient;
+    int32_t ambient_miss;
+};
+
+} // namespace rtc

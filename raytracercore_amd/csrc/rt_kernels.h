@@ -1,0 +1,41 @@
+// rt_kernels.h -- launch interface between the C ABI (rtcore_api.hip) and the kernels.
+#pragma once
+#include "rt_internal.h"
+
+namespace rtc {
+
+// Work decomposition of one path-tracing launch over a w x h tile.
+struct PathParams {
+    int x0, y0, w, h;           // tile within the frame
+    int band, band_stride, band_offset; // band > 0: tile row r is frame row
+                                        // y0 + ((r / band) * band_stride + band_offset) * band + r % band
+    int spp;                    // samples per pixel in this launch
+    int chunk;                  // samples per work item (a lane owns one item at a time)
+    int n_chunks;               // ceil(spp / chunk)
+    int blocks_x;               // 8x8 pixel blocks per tile row
+    int n_pad;                  // padded pixels per chunk (blocks * 64)
+    unsigned long long seed;
+    unsigned long long sample_base;
+    unsigned int* counter;      // work-item dispenser (zeroed before launch)
+    float4* partial;            // [n_chunks][n_pad]: rgb sums, (samples | misses << 16)
+    unsigned long long* rays;   // Scene.RayTrace-equivalents (added to)
+    unsigned long long* stats;  // optional [3]: node visits, triangle tests, sphere tests
+};
+
+hipError_t launch_primary_ids(const DevScene& s, const CameraD& cam, int x0, int y0, int w, int h, int32_t* d_ids,
+                              hipStream_t stream);
+
+// Kernel variant for a traversal mode and BVH depth (the LDS stack must exceed the depth).
+int path_variant(int traversal, int bvh_depth);
+// Launch the persistent kernel; stats counts node visits / primitive tests (slower build).
+hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& p, int variant, int grid_blocks,
+                       hipStream_t stream, bool stats);
+int path_blocks_per_cu(int variant, bool stats);
+
+// partial -> fp64 planar accumulators (d_sum[3][w*h], d_samples, d_misses), added to.
+hipError_t launch_accumulate(const PathParams& p, double* d_sum, uint32_t* d_samples, uint32_t* d_misses,
+                             hipStream_t stream);
+// partial (1 spp) -> DoubleColor[w, h] in x*h + y order, Placeholder(-1) on a miss.
+hipError_t launch_colors_1spp(const PathParams& p, double* d_out, hipStream_t stream);
+
+} // namespace rtc

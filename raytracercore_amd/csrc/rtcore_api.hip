@@ -1,0 +1,805 @@
+// rtcore_api.hip -- the C ABI (include/rtcore.h): scene upload, renders, multi-GPU frame.
+//
+// Replaces the body of the reference's render worker loop (Raytracer.Render,
+// Raytracer.cs:294-330) behind FullRaytracer's GetWorkingTile / OnTileFinished contract
+// (FullRaytracer.cs:210-229); see INTEGRATION.md for the C# P/Invoke side.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "host_scene.h"
+#include "rt_kernels.h"
+
+using namespace rtc;
+
+namespace rtc {
+static thread_local std::string g_error;
+void set_error(const std::string& msg) { g_error = msg; }
+} // namespace rtc
+
+#define HIP_TRY(expr)                                                                                   \
+    do {                                                                                                \
+        hipError_t e_ = (expr);                                                                         \
+        if (e_ != hipSuccess) {                                                                         \
+            set_error(std::string(#expr) + ": " + hipGetErrorString(e_));                               \
+            return e_ == hipErrorOutOfMemory ? RT_ERR_OOM : RT_ERR_HIP;                                 \
+        }                                                                                               \
+    } while (0)
+
+namespace {
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    ~DevBuf() { release(); }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    hipError_t reserve(size_t count)
+    {
+        if (count <= n) return hipSuccess;
+        release();
+        hipError_t e = hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T));
+        if (e == hipSuccess) n = count;
+        return e;
+    }
+    hipError_t upload(const std::vector<T>& v)
+    {
+        hipError_t e = reserve(v.size());
+        if (e != hipSuccess || v.empty()) return e;
+        return hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+    }
+};
+
+float4 f4(Vec4d v, float w) { return make_float4((float)v.x, (float)v.y, (float)v.z, w); }
+float as_f(int v)
+{
+    float f;
+    std::memcpy(&f, &v, 4);
+    return f;
+}
+float as_f(uint32_t v)
+{
+    float f;
+    std::memcpy(&f, &v, 4);
+    return f;
+}
+double luminance(rt_color c) { return 0.299 * c.r + 0.587 * c.g + 0.114 * c.b; } // DoubleColor.cs:76-79
+
+} // namespace
+
+struct rt_scene {
+    int device = 0;
+    int n_cu = 256;
+    rt_scene_params params{};
+    std::vector<HostPrim> host;
+    int traversal = RT_TRAVERSAL_AUTO, resolved = RT_TRAVERSAL_BRUTE;
+    int variant = 0;
+    int blocks_per_cu = 1;
+    RefBvh ref;
+    SahBvh sah;
+    DevScene dev{};
+    DevBuf<PrimF> prims_bf, prims_bvh;
+    DevBuf<NodeF> nodes;
+    DevBuf<XformF> xf;
+    DevBuf<MatF> mats;
+    DevBuf<float4> vnormals;
+    DevBuf<PrimD> prims_d;
+    DevBuf<XformD> xf_d;
+    DevBuf<RefNode> ref_nodes;
+    // work buffers
+    DevBuf<unsigned int> counter;
+    DevBuf<unsigned long long> rays;
+    DevBuf<float4> partial;
+    DevBuf<double> sum, colors;
+    DevBuf<uint32_t> samples, misses;
+    DevBuf<int32_t> ids;
+    CameraD camd{};
+    CameraF camf{};
+    bool has_camera = false;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    uint64_t device_bytes = 0;
+
+    ~rt_scene()
+    {
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+
+int upload_scene(rt_scene* s)
+{
+    const auto& H = s->host;
+    const int n = (int)H.size();
+    // --- exact fp64 set
+    std::vector<PrimD> pd(n);
+    std::vector<XformD> xd;
+    std::vector<float4> vn((size_t)std::max(1, n) * 3, make_float4(0, 0, 0, 0));
+    std::vector<XformF> xf;
+    std::vector<int> xf_index(n, -1);
+    for (int i = 0; i < n; i++) {
+        const HostPrim& p = H[i];
+        PrimD& d = pd[i];
+        std::memset(&d, 0, sizeof d);
+        d.flags = p.flags;
+        d.xf = -1;
+        if (p.kind == RT_PRIM_TRIANGLE) {
+            d.a = p.v[0];
+            d.b = p.e01;
+            d.c = p.e02;
+            d.d = p.n;
+            for (int k = 0; k < 3; k++) {
+                d.vn[k] = p.vn[k];
+                vn[3 * i + k] = f4(p.vn[k], 0.0f);
+            }
+        } else if (p.kind == RT_PRIM_SPHERE) {
+            d.a = p.center;
+            d.b = v4d(p.radius, p.radius_sqr, 0, 0);
+            if (p.flags & F_TRANSFORMED) {
+                d.xf = (int)xd.size();
+                xf_index[i] = (int)xf.size();
+                XformD X;
+                std::memcpy(X.to_world, p.to_world, sizeof X.to_world);
+                std::memcpy(X.to_obj, p.to_obj, sizeof X.to_obj);
+                std::memcpy(X.to_normal, p.to_normal, sizeof X.to_normal);
+                xd.push_back(X);
+                XformF F;
+                for (int r = 0; r < 3; r++) {
+                    F.to_world[r] = make_float4((float)p.to_world[4 * r], (float)p.to_world[4 * r + 1],
+                                                (float)p.to_world[4 * r + 2], (float)p.to_world[4 * r + 3]);
+                    F.to_obj[r] = make_float4((float)p.to_obj[4 * r], (float)p.to_obj[4 * r + 1],
+                                              (float)p.to_obj[4 * r + 2], (float)p.to_obj[4 * r + 3]);
+                    F.to_normal[r] = make_float4((float)p.to_normal[4 * r], (float)p.to_normal[4 * r + 1],
+                                                 (float)p.to_normal[4 * r + 2], (float)p.to_normal[4 * r + 3]);
+                }
+                xf.push_back(F);
+            }
+        } else {
+            d.a = p.pn;
+            d.b = v4d(p.pd, 0, 0, 0);
+        }
+    }
+    // --- fast fp32 set
+    auto primf = [&](int i) {
+        const HostPrim& p = H[i];
+        PrimF f;
+        std::memset(&f, 0, sizeof f);
+        if (p.kind == RT_PRIM_TRIANGLE) {
+            f.a = f4(p.v[0], as_f(i));
+            f.b = f4(p.e01, as_f(p.flags));
+            f.c = f4(p.e02, 0.0f);
+            f.d = f4(p.n, 0.0f);
+        } else if (p.kind == RT_PRIM_SPHERE) {
+            f.a = f4(p.center, as_f(i));
+            f.b = make_float4((float)p.radius, (float)p.radius_sqr, as_f(xf_index[i]), as_f(p.flags));
+        } else {
+            f.a = f4(p.pn, as_f(i));
+            f.b = make_float4((float)p.pd, 0.0f, 0.0f, as_f(p.flags));
+        }
+        return f;
+    };
+    std::vector<PrimF> bf;
+    int nt = 0, ns = 0, np = 0;
+    for (int kind = 0; kind < 3; kind++)
+        for (int i = 0; i < n; i++)
+            if (H[i].kind == kind) {
+                bf.push_back(primf(i));
+                (kind == 0 ? nt : kind == 1 ? ns : np)++;
+            }
+    std::vector<PrimF> bv;
+    for (int i : s->sah.order) bv.push_back(primf(i));
+    std::vector<MatF> mats(n);
+    for (int i = 0; i < n; i++) {
+        const HostPrim& p = H[i];
+        const bool refl = p.shininess > 0; // Primitive.IsReflective (Primitive.cs:107-129)
+        rt_color spec = refl ? p.specular : rt_color{0, 0, 0};
+        rt_color refr = refl ? p.refraction : rt_color{0, 0, 0};
+        MatF& m = mats[i];
+        m.emission = make_float4((float)p.emission.r, (float)p.emission.g, (float)p.emission.b, (float)luminance(p.emission));
+        m.diffuse = make_float4((float)p.diffuse.r, (float)p.diffuse.g, (float)p.diffuse.b, (float)luminance(p.diffuse));
+        m.specular = make_float4((float)spec.r, (float)spec.g, (float)spec.b, (float)luminance(spec));
+        m.refraction = make_float4((float)refr.r, (float)refr.g, (float)refr.b, (float)luminance(refr));
+        m.shininess = (float)p.shininess;
+        m.ior = (float)p.ior;
+        m.flags = p.flags;
+        m.pad = 0;
+    }
+    HIP_TRY(s->prims_d.upload(pd));
+    HIP_TRY(s->xf_d.upload(xd));
+    HIP_TRY(s->ref_nodes.upload(s->ref.nodes));
+    HIP_TRY(s->prims_bf.upload(bf));
+    HIP_TRY(s->prims_bvh.upload(bv));
+    HIP_TRY(s->nodes.upload(s->sah.nodes));
+    HIP_TRY(s->xf.upload(xf));
+    HIP_TRY(s->mats.upload(mats));
+    HIP_TRY(s->vnormals.upload(vn));
+    s->device_bytes = pd.size() * sizeof(PrimD) + xd.size() * sizeof(XformD) + s->ref.nodes.size() * sizeof(RefNode) +
+                      bf.size() * sizeof(PrimF) + bv.size() * sizeof(PrimF) + s->sah.nodes.size() * sizeof(NodeF) +
+                      xf.size() * sizeof(XformF) + mats.size() * sizeof(MatF) + vn.size() * sizeof(float4);
+
+    DevScene& d = s->dev;
+    d.prims_bf = s->prims_bf.p;
+    d.n_tri = nt;
+    d.n_sph = ns;
+    d.n_pln = np;
+    d.prims_bvh = s->prims_bvh.p;
+    d.nodes = s->nodes.p;
+    d.n_nodes = (int)s->sah.nodes.size();
+    d.root = s->sah.root;
+    d.xf = s->xf.p;
+    d.mats = s->mats.p;
+    d.vnormals = s->vnormals.p;
+    d.prims_d = s->prims_d.p;
+    d.xf_d = s->xf_d.p;
+    d.ref_nodes = s->ref_nodes.p;
+    d.n_ref_nodes = (int)s->ref.nodes.size();
+    d.width = s->params.width;
+    d.height = s->params.height;
+    d.recursion = s->params.recursion;
+    d.debug_geom = s->params.debug_geom;
+    d.air_ior = (float)s->params.air_ior;
+    const rt_color& a = s->params.ambient;
+    d.ambient = make_float3((float)a.r, (float)a.g, (float)a.b);
+    d.ambient_miss = (a.r == -1 && a.g == -1 && a.b == -1) ? 1 : 0; // AmbientRGB == Placeholder
+    return RT_OK;
+}
+
+int resolve_traversal(rt_scene* s)
+{
+    int t = s->traversal;
+    if (t == RT_TRAVERSAL_AUTO) t = (s->dev.n_tri + s->dev.n_sph) <= 48 ? RT_TRAVERSAL_BRUTE : RT_TRAVERSAL_BVH;
+    if (t == RT_TRAVERSAL_BVH && s->sah.depth >= 48) {
+        set_error("BVH deeper than the kernel's LDS stack");
+        return RT_ERR_ARG;
+    }
+    s->resolved = t;
+    s->variant = path_variant(t, s->sah.depth);
+    s->blocks_per_cu = path_blocks_per_cu(s->variant, false);
+    return RT_OK;
+}
+
+PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint64_t seed, uint64_t base)
+{
+    PathParams p{};
+    p.x0 = x0;
+    p.y0 = y0;
+    p.w = w;
+    p.h = h;
+    p.band = 0;
+    p.spp = spp;
+    // about 8 chunks per pixel keeps the tail of a launch short while each lane still
+    // amortises its item fetch over several samples
+    p.chunk = std::max(1, std::min(64, (spp + 7) / 8));
+    p.n_chunks = (spp + p.chunk - 1) / p.chunk;
+    p.blocks_x = (w + 7) / 8;
+    p.n_pad = p.blocks_x * ((h + 7) / 8) * 64;
+    p.seed = seed;
+    p.sample_base = base;
+    return p;
+}
+
+int check_tile(rt_scene* s, int x0, int y0, int w, int h)
+{
+    if (!s) {
+        set_error("null scene");
+        return RT_ERR_ARG;
+    }
+    if (!s->has_camera) {
+        set_error("no camera set (rt_scene_set_camera)");
+        return RT_ERR_STATE;
+    }
+    if (w <= 0 || h <= 0 || x0 < 0 || y0 < 0 || x0 + w > s->params.width || y0 + h > s->params.height) {
+        set_error("tile outside the frame");
+        return RT_ERR_ARG;
+    }
+    return RT_OK;
+}
+
+// Launch the path kernel for p (work buffers sized here), timing it with the scene's events.
+int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t stream)
+{
+    const size_t need = (size_t)p.n_chunks * (size_t)p.n_pad;
+    HIP_TRY(s->partial.reserve(need));
+    HIP_TRY(s->counter.reserve(1));
+    p.partial = s->partial.p;
+    p.counter = s->counter.p;
+    p.rays = d_rays;
+    p.stats = nullptr;
+    HIP_TRY(hipMemsetAsync(p.counter, 0, sizeof(unsigned int), stream));
+    int grid = s->n_cu * s->blocks_per_cu;
+    HIP_TRY(hipEventRecord(s->ev0, stream));
+    HIP_TRY(launch_path(s->dev, s->camf, p, s->variant, grid, stream, false));
+    HIP_TRY(hipEventRecord(s->ev1, stream));
+    return RT_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return RTCORE_ABI_VERSION; }
+
+int rt_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int rt_last_error(char* buf, int32_t cap)
+{
+    if (buf && cap > 0) {
+        std::strncpy(buf, g_error.c_str(), (size_t)cap - 1);
+        buf[cap - 1] = 0;
+    }
+    return (int)g_error.size();
+}
+
+int rt_scene_create(const rt_scene_params* params, const rt_prim* prims, int32_t n_prims, int32_t device,
+                    rt_scene** out_scene)
+{
+    if (!params || !out_scene || n_prims < 0 || (n_prims > 0 && !prims)) {
+        set_error("rt_scene_create: bad argument");
+        return RT_ERR_ARG;
+    }
+    *out_scene = nullptr;
+    if (params->width <= 0 || params->height <= 0) {
+        set_error("rt_scene_create: width and height must be positive");
+        return RT_ERR_ARG;
+    }
+    for (int i = 0; i < n_prims; i++)
+        if (prims[i].kind < 0 || prims[i].kind > 2) {
+            set_error("rt_scene_create: unknown primitive kind at index " + std::to_string(i));
+            return RT_ERR_ARG;
+        }
+    int ndev = rt_device_count();
+    if (ndev <= 0) {
+        set_error("rt_scene_create: no HIP device");
+        return RT_ERR_NODEVICE;
+    }
+    if (device < 0 || device >= ndev) {
+        set_error("rt_scene_create: device index out of range");
+        return RT_ERR_ARG;
+    }
+    std::unique_ptr<rt_scene> s(new rt_scene());
+    s->device = device;
+    s->params = *params;
+    HIP_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    s->n_cu = prop.multiProcessorCount;
+    HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&s->ev0));
+    HIP_TRY(hipEventCreate(&s->ev1));
+    s->host = prepare_prims(prims, n_prims);
+    s->ref = build_ref_bvh(s->host);
+    s->sah = build_sah_bvh(s->host, n_prims > 256 ? 4 : 2);
+    int rc = upload_scene(s.get());
+    if (rc != RT_OK) return rc;
+    rc = resolve_traversal(s.get());
+    if (rc != RT_OK) return rc;
+    HIP_TRY(s->rays.reserve(1));
+    *out_scene = s.release();
+    return RT_OK;
+}
+
+int rt_scene_set_camera(rt_scene* s, const rt_camera* cam)
+{
+    if (!s || !cam || (cam->kind != RT_CAMERA_FRUSTUM && cam->kind != RT_CAMERA_ORTHO)) {
+        set_error("rt_scene_set_camera: bad argument");
+        return RT_ERR_ARG;
+    }
+    camera_init(*cam, s->params.width, s->params.height, s->camd, s->camf);
+    s->has_camera = true;
+    return RT_OK;
+}
+
+int rt_scene_set_traversal(rt_scene* s, int32_t traversal)
+{
+    if (!s || traversal < RT_TRAVERSAL_AUTO || traversal > RT_TRAVERSAL_BVH) {
+        set_error("rt_scene_set_traversal: bad argument");
+        return RT_ERR_ARG;
+    }
+    HIP_TRY(hipSetDevice(s->device));
+    s->traversal = traversal;
+    return resolve_traversal(s);
+}
+
+int rt_scene_get_info(const rt_scene* s, rt_scene_info* info)
+{
+    if (!s || !info) {
+        set_error("rt_scene_get_info: bad argument");
+        return RT_ERR_ARG;
+    }
+    std::memset(info, 0, sizeof *info);
+    info->n_prims = (int32_t)s->host.size();
+    info->ref_bvh_nodes = (int32_t)s->ref.nodes.size();
+    info->ref_bvh_depth = s->ref.depth;
+    info->sah_bvh_nodes = (int32_t)s->sah.nodes.size();
+    info->sah_bvh_depth = s->sah.depth;
+    info->traversal = s->resolved;
+    info->device = s->device;
+    info->device_bytes = s->device_bytes;
+    return RT_OK;
+}
+
+void rt_scene_destroy(rt_scene* s)
+{
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    (void)hipStreamSynchronize(s->stream);
+    delete s;
+}
+
+int rt_render_device(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t spp, uint64_t seed,
+                     uint64_t sample_base, double* d_sum, uint32_t* d_samples, uint32_t* d_misses,
+                     unsigned long long* d_rays, void* stream)
+{
+    int rc = check_tile(s, x0, y0, w, h);
+    if (rc != RT_OK) return rc;
+    if (spp <= 0 || !d_sum || !d_samples || !d_misses || !d_rays) {
+        set_error("rt_render_device: bad argument");
+        return RT_ERR_ARG;
+    }
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    PathParams p = make_params(s, x0, y0, w, h, spp, seed, sample_base);
+    rc = run_path(s, p, d_rays, st);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(launch_accumulate(p, d_sum, d_samples, d_misses, st));
+    return RT_OK;
+}
+
+int rt_last_kernel_ms(rt_scene* s, float* ms)
+{
+    if (!s || !ms) {
+        set_error("rt_last_kernel_ms: bad argument");
+        return RT_ERR_ARG;
+    }
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipEventSynchronize(s->ev1));
+    HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
+    return RT_OK;
+}
+
+int rt_render_tile(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t spp, uint64_t seed,
+                   uint64_t sample_base, rt_color* sum_rgb, uint32_t* samples, uint32_t* misses, uint64_t* rays_out)
+{
+    int rc = check_tile(s, x0, y0, w, h);
+    if (rc != RT_OK) return rc;
+    if (spp < 0 || !sum_rgb || !samples || !misses) {
+        set_error("rt_render_tile: bad argument");
+        return RT_ERR_ARG;
+    }
+    if (spp == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    const size_t npix = (size_t)w * h;
+    HIP_TRY(s->sum.reserve(3 * npix));
+    HIP_TRY(s->samples.reserve(npix));
+    HIP_TRY(s->misses.reserve(npix));
+    HIP_TRY(hipMemsetAsync(s->sum.p, 0, 3 * npix * sizeof(double), s->stream));
+    HIP_TRY(hipMemsetAsync(s->samples.p, 0, npix * sizeof(uint32_t), s->stream));
+    HIP_TRY(hipMemsetAsync(s->misses.p, 0, npix * sizeof(uint32_t), s->stream));
+    HIP_TRY(hipMemsetAsync(s->rays.p, 0, sizeof(unsigned long long), s->stream));
+    rc = rt_render_device(s, x0, y0, w, h, spp, seed, sample_base, s->sum.p, s->samples.p, s->misses.p, s->rays.p,
+                          s->stream);
+    if (rc != RT_OK) return rc;
+    std::vector<double> hs(3 * npix);
+    std::vector<uint32_t> hn(npix), hm(npix);
+    unsigned long long hr = 0;
+    HIP_TRY(hipMemcpyAsync(hs.data(), s->sum.p, hs.size() * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipMemcpyAsync(hn.data(), s->samples.p, npix * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipMemcpyAsync(hm.data(), s->misses.p, npix * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipMemcpyAsync(&hr, s->rays.p, sizeof hr, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            const size_t i = (size_t)y * w + x, o = (size_t)x * h + y; // device row-major -> C# [x, y]
+            sum_rgb[o].r += hs[i];
+            sum_rgb[o].g += hs[npix + i];
+            sum_rgb[o].b += hs[2 * npix + i];
+            samples[o] += hn[i];
+            misses[o] += hm[i];
+        }
+    if (rays_out) *rays_out += hr;
+    return RT_OK;
+}
+
+int rt_render_tile_1spp(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, uint64_t seed,
+                        uint64_t sample_index, rt_color* out)
+{
+    int rc = check_tile(s, x0, y0, w, h);
+    if (rc != RT_OK) return rc;
+    if (!out) {
+        set_error("rt_render_tile_1spp: bad argument");
+        return RT_ERR_ARG;
+    }
+    HIP_TRY(hipSetDevice(s->device));
+    const size_t npix = (size_t)w * h;
+    HIP_TRY(s->colors.reserve(3 * npix));
+    HIP_TRY(hipMemsetAsync(s->rays.p, 0, sizeof(unsigned long long), s->stream));
+    PathParams p = make_params(s, x0, y0, w, h, 1, seed, sample_index);
+    rc = run_path(s, p, s->rays.p, s->stream);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(launch_colors_1spp(p, s->colors.p, s->stream));
+    HIP_TRY(hipMemcpyAsync(out, s->colors.p, npix * sizeof(rt_color), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return RT_OK;
+}
+
+int rt_primary_ids_device(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t* d_ids, void* stream)
+{
+    int rc = check_tile(s, x0, y0, w, h);
+    if (rc != RT_OK) return rc;
+    if (!d_ids) {
+        set_error("rt_primary_ids_device: bad argument");
+        return RT_ERR_ARG;
+    }
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(launch_primary_ids(s->dev, s->camd, x0, y0, w, h, d_ids, static_cast<hipStream_t>(stream)));
+    return RT_OK;
+}
+
+int rt_primary_ids(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t* ids_out)
+{
+    int rc = check_tile(s, x0, y0, w, h);
+    if (rc != RT_OK) return rc;
+    if (!ids_out) {
+        set_error("rt_primary_ids: bad argument");
+        return RT_ERR_ARG;
+    }
+    HIP_TRY(hipSetDevice(s->device));
+    const size_t npix = (size_t)w * h;
+    HIP_TRY(s->ids.reserve(npix));
+    rc = rt_primary_ids_device(s, x0, y0, w, h, s->ids.p, s->stream);
+    if (rc != RT_OK) return rc;
+    std::vector<int32_t> tmp(npix);
+    HIP_TRY(hipMemcpyAsync(tmp.data(), s->ids.p, npix * sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    bool overflow = false;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            int32_t v = tmp[(size_t)y * w + x];
+            overflow |= v == -2;
+            ids_out[(size_t)x * h + y] = v;
+        }
+    if (overflow) {
+        set_error("rt_primary_ids: a ray pierced more leaves than the exact kernel's list holds");
+        return RT_ERR_STATE;
+    }
+    return RT_OK;
+}
+
+int rt_render_frame_multi(const rt_scene_params* params, const rt_prim* prims, int32_t n_prims,
+                          const rt_camera* camera, int32_t n_gpus, int32_t spp, uint64_t seed, rt_color* sum_rgb,
+                          uint32_t* samples, uint32_t* misses, uint64_t* rays_out)
+{
+    if (!params || !camera || !sum_rgb || !samples || !misses || spp <= 0 || n_gpus <= 0) {
+        set_error("rt_render_frame_multi: bad argument");
+        return RT_ERR_ARG;
+    }
+    int ndev = rt_device_count();
+    if (n_gpus > ndev) {
+        set_error("rt_render_frame_multi: not enough devices");
+        return RT_ERR_NODEVICE;
+    }
+    const int W = params->width, H = params->height, band = 16;
+    const int n_bands = (H + band - 1) / band;
+    // device g owns bands g, g + n, g + 2n, ... (row-interleaved for load balance)
+    std::vector<int> rows(n_gpus, 0);
+    for (int b = 0; b < n_bands; b++) rows[b % n_gpus] += std::min(band, H - b * band);
+    const int max_rows = *std::max_element(rows.begin(), rows.end());
+    const size_t slot_pix = (size_t)max_rows * W;
+    const size_t slot_bytes = slot_pix * (3 * sizeof(double) + 2 * sizeof(uint32_t));
+
+    std::vector<rt_scene*> scenes(n_gpus, nullptr);
+    std::vector<ncclComm_t> comms(n_gpus);
+    std::vector<int> devs(n_gpus);
+    std::vector<unsigned char*> sendb(n_gpus, nullptr);
+    unsigned char* recvb = nullptr;
+    int rc = RT_OK;
+    auto cleanup = [&]() {
+        for (int g = 0; g < n_gpus; g++) {
+            if (sendb[g]) {
+                (void)hipSetDevice(g);
+                (void)hipFree(sendb[g]);
+            }
+            if (scenes[g]) rt_scene_destroy(scenes[g]);
+        }
+        if (recvb) {
+            (void)hipSetDevice(0);
+            (void)hipFree(recvb);
+        }
+    };
+    for (int g = 0; g < n_gpus; g++) {
+        devs[g] = g;
+        rc = rt_scene_create(params, prims, n_prims, g, &scenes[g]);
+        if (rc == RT_OK) rc = rt_scene_set_camera(scenes[g], camera);
+        if (rc != RT_OK) {
+            cleanup();
+            return rc;
+        }
+        (void)hipSetDevice(g);
+        if (hipMalloc(&sendb[g], slot_bytes) != hipSuccess || hipMemset(sendb[g], 0, slot_bytes) != hipSuccess) {
+            set_error("rt_render_frame_multi: device allocation failed");
+            cleanup();
+            return RT_ERR_OOM;
+        }
+    }
+    (void)hipSetDevice(0);
+    if (hipMalloc(&recvb, slot_bytes * n_gpus) != hipSuccess) {
+        set_error("rt_render_frame_multi: device allocation failed");
+        cleanup();
+        return RT_ERR_OOM;
+    }
+    if (ncclCommInitAll(comms.data(), n_gpus, devs.data()) != ncclSuccess) {
+        set_error("rt_render_frame_multi: ncclCommInitAll failed");
+        cleanup();
+        return RT_ERR_NCCL;
+    }
+    std::vector<unsigned long long> hrays(n_gpus, 0);
+    for (int g = 0; g < n_gpus && rc == RT_OK; g++) {
+        rt_scene* s = scenes[g];
+        (void)hipSetDevice(g);
+        double* d_sum = reinterpret_cast<double*>(sendb[g]);
+        uint32_t* d_n = reinterpret_cast<uint32_t*>(d_sum + 3 * slot_pix);
+        uint32_t* d_m = d_n + slot_pix;
+        if (rows[g] == 0) continue;
+        (void)hipMemsetAsync(s->rays.p, 0, sizeof(unsigned long long), s->stream);
+        PathParams p = make_params(s, 0, 0, W, rows[g], spp, seed, 0);
+        p.band = band;
+        p.band_stride = n_gpus;
+        p.band_offset = g;
+        rc = run_path(s, p, s->rays.p, s->stream);
+        if (rc == RT_OK && launch_accumulate(p, d_sum, d_n, d_m, s->stream) != hipSuccess) rc = RT_ERR_HIP;
+    }
+    if (rc == RT_OK) {
+        ncclGroupStart();
+        for (int g = 0; g < n_gpus; g++) {
+            (void)hipSetDevice(g);
+            if (ncclGather(sendb[g], g == 0 ? recvb : nullptr, slot_bytes, ncclUint8, 0, comms[g], scenes[g]->stream) !=
+                ncclSuccess)
+                rc = RT_ERR_NCCL;
+        }
+        if (ncclGroupEnd() != ncclSuccess) rc = RT_ERR_NCCL;
+    }
+    std::vector<unsigned char> host;
+    if (rc == RT_OK) {
+        for (int g = 0; g < n_gpus; g++) {
+            (void)hipSetDevice(g);
+            (void)hipMemcpyAsync(&hrays[g], scenes[g]->rays.p, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                 scenes[g]->stream);
+            if (hipStreamSynchronize(scenes[g]->stream) != hipSuccess) rc = RT_ERR_HIP;
+        }
+        host.resize(slot_bytes * n_gpus);
+        (void)hipSetDevice(0);
+        if (hipMemcpy(host.data(), recvb, host.size(), hipMemcpyDeviceToHost) != hipSuccess) rc = RT_ERR_HIP;
+    }
+    for (int g = 0; g < n_gpus; g++) ncclCommDestroy(comms[g]);
+    if (rc == RT_OK) {
+        std::vector<int> seen(n_gpus, 0);
+        for (int b = 0; b < n_bands; b++) {
+            const int g = b % n_gpus;
+            const unsigned char* base = host.data() + slot_bytes * g;
+            const double* hs = reinterpret_cast<const double*>(base);
+            const uint32_t* hn = reinterpret_cast<const uint32_t*>(hs + 3 * slot_pix);
+            const uint32_t* hm = hn + slot_pix;
+            for (int r = 0; r < std::min(band, H - b * band); r++) {
+                const int tr = seen[g]++, y = b * band + r;
+                for (int x = 0; x < W; x++) {
+                    const size_t i = (size_t)tr * W + x, o = (size_t)x * H + y;
+                    sum_rgb[o].r += hs[i];
+                    sum_rgb[o].g += hs[slot_pix + i];
+                    sum_rgb[o].b += hs[2 * slot_pix + i];
+                    samples[o] += hn[i];
+                    misses[o] += hm[i];
+                }
+            }
+        }
+        if (rays_out)
+            for (auto r : hrays) *rays_out += r;
+    } else if (g_error.empty()) {
+        set_error("rt_render_frame_multi failed");
+    }
+    cleanup();
+    return rc;
+}
+
+int rt_parse_scene(const char* text, rt_scene_params* params, rt_prim* prims, int32_t* n_prims, rt_camera* cameras,
+                   int32_t* n_cameras)
+{
+    if (!text || !n_prims || !n_cameras) {
+        set_error("rt_parse_scene: bad argument");
+        return RT_ERR_ARG;
+    }
+    ParsedScene ps;
+    std::string err;
+    if (!parse_scene_text(text, ps, err)) {
+        set_error(err);
+        return RT_ERR_PARSE;
+    }
+    const int cap_p = *n_prims, cap_c = *n_cameras;
+    *n_prims = (int32_t)ps.prims.size();
+    *n_cameras = (int32_t)ps.cameras.size();
+    if (params) *params = ps.params;
+    if (prims) {
+        if (cap_p < (int)ps.prims.size()) {
+            set_error("rt_parse_scene: primitive array too small");
+            return RT_ERR_ARG;
+        }
+        std::copy(ps.prims.begin(), ps.prims.end(), prims);
+    }
+    if (cameras) {
+        if (cap_c < (int)ps.cameras.size()) {
+            set_error("rt_parse_scene: camera array too small");
+            return RT_ERR_ARG;
+        }
+        std::copy(ps.cameras.begin(), ps.cameras.end(), cameras);
+    }
+    return RT_OK;
+}
+
+int rt_ref_bvh_export(const rt_prim* prims, int32_t n, int32_t* leaf_order, double* boxes, int32_t* n_nodes,
+                      int32_t* depth)
+{
+    if (n < 0 || (n > 0 && !prims)) {
+        set_error("rt_ref_bvh_export: bad argument");
+        return RT_ERR_ARG;
+    }
+    std::vector<HostPrim> host = prepare_prims(prims, n);
+    RefBvh ref = build_ref_bvh(host);
+    int k = 0;
+    for (size_t i = 0; i < ref.nodes.size(); i++) {
+        const RefNode& r = ref.nodes[i];
+        if (r.prim >= 0 && leaf_order) leaf_order[k++] = r.prim;
+        if (boxes) {
+            double* b = boxes + 8 * i;
+            b[0] = r.mn.x; b[1] = r.mn.y; b[2] = r.mn.z; b[3] = r.mn.w;
+            b[4] = r.mx.x; b[5] = r.mx.y; b[6] = r.mx.z; b[7] = r.mx.w;
+        }
+    }
+    if (n_nodes) *n_nodes = (int32_t)ref.nodes.size();
+    if (depth) *depth = ref.depth;
+    return RT_OK;
+}
+
+int32_t rt_sample_output(rt_color sum, uint32_t n_samples, uint32_t n_misses, rt_color back, double back_alpha,
+                         double exposure)
+{
+    // SampleSet.GetOutput / GetColorCode (SampleSet.cs:50-113) with Util.Clamp's SSE form
+    auto clamp01 = [](double v) {
+        v = v > 0.0 ? v : 0.0;
+        return v < 1.0 ? v : 1.0;
+    };
+    auto code = [&](double r, double g, double b, double a) {
+        return (int32_t)(((uint32_t)(int32_t)(clamp01(a) * 255) << 24) | ((uint32_t)(int32_t)(clamp01(r) * 255) << 16) |
+                         ((uint32_t)(int32_t)(clamp01(g) * 255) << 8) | (uint32_t)(int32_t)(clamp01(b) * 255));
+    };
+    if (n_samples == 0) return code(back.r * exposure, back.g * exposure, back.b * exposure, back_alpha);
+    double total = (double)n_samples + (double)n_misses;
+    double mult = exposure / n_samples;
+    double r = sum.r * mult, g = sum.g * mult, b = sum.b * mult, a = 1;
+    double bam = n_misses / total, bk = bam * back_alpha;
+    r += (back.r - r) * bk;
+    g += (back.g - g) * bk;
+    b += (back.b - b) * bk;
+    a += (back_alpha - a) * bam;
+    const double gamma = 1 / 2.2;
+    return code(pow(r, gamma), pow(g, gamma), pow(b, gamma), a);
+}
+
+} // extern "C"

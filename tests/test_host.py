@@ -1,0 +1,147 @@
+"""Host side of the library, no GPU needed: the C ABI exports, the scene loader and the
+reference-BVH build, each checked bit for bit against the oracle's independent restatement.
+"""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle.oracle import OracleScene, sample_output as orc_sample_output
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_functions():
+    text = open(os.path.join(ROOT, "include", "rtcore.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|void|int32_t)\s+(rt_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_library_exports_every_declared_symbol(rc):
+    lib = rc.load_library()
+    names = _declared_functions()
+    assert len(names) >= 18
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", rc.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (rt_\w+)", out))
+    assert set(names) <= exported
+    assert lib.rt_abi_version() == 1
+
+
+def test_library_has_gfx950_code_object(rc):
+    blob = open(rc.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob, "librtcore_hip.so carries no gfx950 code object"
+
+
+SYNTH = """size 64 48
+recursion 5
+ambient color .1 .2 .3
+dof .05 3 at 0 0 0
+camera 0 -4 1, 0 0 0, 0 0 1, 50
+orthographic 0 -4 1 0 0 0 0 0 1 3
+pushtransform
+translate .5 -.25 .1
+rotate 1 2 3 30
+scale 1 2 .5
+shininess 10 2
+emission .5 .4 .3
+sphere 0 0 0 .7
+cube 0 0 0 1 1 1 not -x +z
+poptransform
+refraction .8 .8 .8, 1.33
+twosided no
+vertex 0 0 0
+vertex 1 0 0
+vertex 0 1 .2
+tri 0 1 2
+tri 0 2 1 mirrored
+refraction off
+vertexnormal 0 0 1 0 0 1
+vertexnormal 1 0 1 0 1 1
+vertexnormal 0 1 1 1 0 1
+trinormal 0 1 2
+plane 2 0 0 1   # comment
+debug off
+"""
+
+
+def _bytes(arr):
+    return [bytes(x) for x in arr]
+
+
+@pytest.mark.parametrize("name", ["bounce.txt", "die.txt", "SYNTH"])
+def test_loader_matches_oracle(rc, name):
+    text = SYNTH if name == "SYNTH" else open(rc.scene_path(name)).read()
+    ps = rc.SceneLoader.from_text(text)
+    orc = OracleScene.from_text(text)
+    params, prims, cams = orc.export()
+    assert ps.n_prims == orc.n_prims and len(ps.cameras) == orc.n_cameras
+    assert bytes(ps.params) == bytes(params)
+    assert _bytes(ps.prims) == _bytes(prims)
+    assert _bytes(ps.cameras) == _bytes(cams)
+
+
+@pytest.mark.parametrize("name", ["bounce.txt", "die.txt", "SYNTH"])
+def test_reference_bvh_matches_oracle(rc, name):
+    text = SYNTH if name == "SYNTH" else open(rc.scene_path(name)).read()
+    ps = rc.SceneLoader.from_text(text)
+    orc = OracleScene.from_text(text)
+    order, boxes, nodes, depth = rc.ref_bvh_export(list(ps.prims))
+    assert (nodes, depth) == orc.bvh_info()
+    assert np.array_equal(order, orc.bvh_leaf_order())
+    b2 = orc.bvh_boxes()
+    assert np.array_equal(boxes, b2) or np.array_equal(np.isnan(boxes), np.isnan(b2))
+
+
+@pytest.mark.parametrize("n,seed", [(5, 1), (20, 2), (21, 3), (64, 4), (300, 5)])
+def test_reference_bvh_regimes(rc, n, seed):
+    """Brute force (n <= 20) and heap agglomeration (21..200000) agree with the oracle."""
+    rng = np.random.default_rng(seed)
+    lines = ["size 16 16", "camera 0 0 -10 0 0 0 0 1 0 60"]
+    nv = 0
+    for i in range(n):
+        c = rng.uniform(-5, 5, 3)
+        if rng.random() < 0.5:
+            lines.append("sphere %.6f %.6f %.6f %.4f" % (c[0], c[1], c[2], rng.uniform(0.05, 0.8)))
+        else:
+            for _ in range(3):
+                v = c + rng.uniform(-0.7, 0.7, 3)
+                lines.append("vertex %.6f %.6f %.6f" % tuple(v))
+            lines.append("tri %d %d %d" % (nv, nv + 1, nv + 2))
+            nv += 3
+    # duplicated centres stress the k-d tree's introsort ties
+    lines.append("sphere 1 1 1 .2")
+    lines.append("sphere 1 1 1 .3")
+    text = "\n".join(lines)
+    ps = rc.SceneLoader.from_text(text)
+    orc = OracleScene.from_text(text)
+    assert _bytes(ps.prims) == _bytes(orc.export()[1])
+    order, boxes, nodes, depth = rc.ref_bvh_export(list(ps.prims))
+    assert (nodes, depth) == orc.bvh_info()
+    assert np.array_equal(order, orc.bvh_leaf_order())
+
+
+@pytest.mark.parametrize("bad", ["size 10", "camera 1 2 3", "cube 0 0 0 1 1 1 some", "instance x",
+                                 "tri 0 1 2", "sphere 1,2 3 4", "size 1.5 2", "ambient foo", "  ,x"])
+def test_loader_errors(rc, bad):
+    with pytest.raises(rc.RtError):
+        rc.SceneLoader.from_text(bad + "\n")
+    with pytest.raises(ValueError):
+        OracleScene.from_text(bad + "\n")
+
+
+def test_loader_ignores_unknown_and_comments(rc):
+    ps = rc.SceneLoader.from_text("# comment\n\n   \noutput x.png\npoint 0 0 0 1 1 1\nmaxverts 3\n")
+    assert ps.n_prims == 0 and len(ps.cameras) == 0
+    assert ps.params.recursion == 3 and ps.params.air_ior == 1.000293
+
+
+@pytest.mark.parametrize("args", [((1.0, 0.5, 0.25), 4, 1, (0, 0, 0), 0.0, 1.0), ((3, 3, 3), 2, 0, (0, 0, 0), 0, 1.7),
+                                  ((0.2, 0.1, 0.05), 1, 3, (0.5, 0.2, 0.9), 0.8, 1.0), ((0, 0, 0), 0, 3, (1, 1, 1), 1, 2),
+                                  ((-1, -1, -1), 1, 0, (0, 0, 0), 0, 1)])
+def test_sample_output_matches_oracle(rc, args):
+    assert rc.sample_output(*args) == orc_sample_output(*args)

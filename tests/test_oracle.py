@@ -1,0 +1,125 @@
+"""The CPU oracle against known answers, its committed golden vectors, and loader facts.
+
+The reference ships no tests or fixtures, so the known answers here are
+analytic (Fresnel at normal incidence, the TIR critical angle, exact sphere and
+parallelogram hits) or follow from the scene files and the loader semantics
+(primitive counts and ID order, BVH node counts).
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from oracle.oracle import OracleScene, fresnel, sample_output
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _scene(name):
+    return OracleScene.from_file(os.path.join(GOLDEN, "scenes", name))
+
+
+def test_fresnel_normal_incidence():
+    # Raytracer.cs:136-153 at cos = 1, air (Scene.cs:35) -> glass 1.52 (bounce.txt:104)
+    r0 = ((1.52 - 1.000293) / (1.52 + 1.000293)) ** 2
+    assert fresnel(1.0, 1.000293, 1.52) == pytest.approx(r0, rel=1e-14)
+    assert r0 == pytest.approx(0.0425221354, rel=1e-9)
+
+
+def test_total_internal_reflection_angle():
+    crit = math.asin(1.000293 / 1.52)
+    assert math.degrees(crit) == pytest.approx(41.154, abs=1e-3)
+    # inside the glass: beyond the critical angle the ratio is 1 (TIR), just inside it is < 1
+    assert fresnel(math.cos(crit + 1e-6), 1.52, 1.000293) == 1.0
+    assert fresnel(math.cos(crit - 1e-4), 1.52, 1.000293) < 1.0
+
+
+SPHERE_SCENE = """size 8 8
+camera 0 0 -5 0 0 0 0 1 0 45
+sphere 0 0 0 1
+"""
+
+
+def test_sphere_hit_exact():
+    s = OracleScene.from_text(SPHERE_SCENE)
+    pid, dist = s.raytrace((0, 0, -5, 1), (0, 0, 1, 0))
+    assert pid == 0 and dist == 4.0
+    pid, dist = s.raytrace((0, 0, 0, 1), (0, 0, 1, 0))  # from the centre: the far root
+    assert pid == 0 and dist == 1.0
+    pid, _ = s.raytrace((0, 2, -5, 1), (0, 0, 1, 0))
+    assert pid == -1
+
+
+def test_parallelogram_hit():
+    # cube face +z of a unit cube at the origin: z = 0.5, u, v in [0, 1]^2 (Triangle.cs:13-20)
+    s = OracleScene.from_text("size 8 8\ncamera 0 0 5 0 0 0 0 1 0 45\ncube 0 0 0 1 1 1 only +z\n")
+    pid, dist = s.raytrace((0.4, 0.4, 5, 1), (0, 0, -1, 0))
+    assert pid == 0 and dist == pytest.approx(4.5, rel=1e-15)
+    pid, _ = s.raytrace((0.6, 0.4, 5, 1), (0, 0, -1, 0))  # just outside the square
+    assert pid == -1
+
+
+def test_one_sided_inverted_room():
+    # bounce.txt's room faces are `invert true` + `twosided false`: seen from outside they
+    # are culled (Primitive.cs:60-64), so camera 0 looks through the near walls
+    s = OracleScene.from_text("size 8 8\ncamera 0 0 5 0 0 0 0 1 0 45\ntwosided false\ninvert true\n"
+                              "cube 0 0 0 2 2 2 all\n")
+    pid, dist = s.raytrace((0, 0, 5, 1), (0, 0, -1, 0))
+    assert pid == 5 and dist == pytest.approx(5.0 + 1.0)  # the far (-z) face, seen from inside
+
+
+@pytest.mark.parametrize("name,prims,nodes,cams", [("bounce.txt", 22, 43, 8), ("die.txt", 29, 57, 3)])
+def test_scene_facts(name, prims, nodes, cams):
+    s = _scene(name)
+    assert s.n_prims == prims and s.n_cameras == cams
+    assert s.bvh_info()[0] == nodes  # 2n - 1 nodes
+    p, pr, c = s.export()
+    kinds = [q.kind for q in pr]
+    if name == "bounce.txt":
+        assert kinds.count(0) == 19 and kinds.count(1) == 3 and (p.width, p.height, p.recursion) == (700, 700, 10)
+        assert pr[20].flags & 16 and pr[20].refractive_index == 1.52  # the lens: transformed sphere
+        assert all(pr[i].emission.r == 5 for i in range(5))  # light box faces 0-4
+        assert all(pr[i].flags & 4 and not pr[i].flags & 2 for i in range(5, 11))  # room: invert, one-sided
+    else:
+        assert kinds.count(0) == 6 and kinds.count(1) == 23 and (p.width, p.height, p.recursion) == (1280, 960, 3)
+        assert c[0].dof_amount == 1000 and c[0].image_plane == pytest.approx(0.1) and c[0].focal_length == 3
+        assert all(q.refractive_index == 0 for q in pr)  # no refraction in die.txt (SURVEY finding 5)
+
+
+@pytest.mark.parametrize("name", ["bounce", "die"])
+def test_golden_primary_ids(name):
+    s = _scene(name + ".txt")
+    s.set_size(64, 64)
+    ref = np.load(os.path.join(GOLDEN, f"primary_ids_{name}_64x64.npy"))
+    assert np.array_equal(s.primary_ids(), ref)
+
+
+@pytest.mark.parametrize("name", ["bounce", "die"])
+def test_golden_accumulators(name):
+    s = _scene(name + ".txt")
+    s.set_size(32, 32)
+    ref = np.load(os.path.join(GOLDEN, f"accum_{name}_32x32_16spp_seed0.npz"))
+    got = s.render_tile(0, 0, 32, 32, 16, seed=0, sample_base=0)
+    assert np.array_equal(got[0], ref["sum"]) and np.array_equal(got[1], ref["samples"])
+    assert np.array_equal(got[2], ref["misses"]) and got[3] == int(ref["rays"][0])
+
+
+def test_sample_output_tonemap():
+    # SampleSet.GetOutput: no samples -> background; gamma 1/2.2; misses blend alpha
+    assert sample_output((0, 0, 0), 0, 5, (0, 0, 0), 0.0, 1.0) == 0
+    c = sample_output((2.0, 2.0, 2.0), 4, 0) & 0xFFFFFFFF
+    v = int(0.5 ** (1 / 2.2) * 255)
+    assert c == (255 << 24) | (v << 16) | (v << 8) | v
+    c = sample_output((4.0, 0, 0), 4, 4) & 0xFFFFFFFF
+    assert (c >> 24) == int(0.5 * 255) and ((c >> 16) & 255) == 255
+
+
+def test_threaded_frame_matches_sequential():
+    """FullRaytracer-style tiling (1 spp per pass) gives the same per-pixel samples."""
+    s = _scene("die.txt")
+    s.set_size(40, 30)
+    a = s.render_frame(3, seed=2, threads=4)
+    b = s.render_tile(0, 0, 40, 30, 3, seed=2)
+    assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and a[3] == b[3]
+    assert np.allclose(a[0], b[0], rtol=1e-12, atol=0)
