@@ -121,8 +121,10 @@ def main() -> int:
     d_rays = torch.zeros(1, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
+    from raytracercore_amd.sharding import merge_accumulators, sample_base
+
     def step(k: int) -> None:
-        base = (k * world + rank) * spp
+        base = sample_base(k, rank, world, spp)
         d_sum.zero_()
         d_n.zero_()
         d_m.zero_()
@@ -130,10 +132,7 @@ def main() -> int:
                           d_rays.data_ptr(), stream)
 
     def merge() -> None:
-        if world > 1:
-            dist.reduce(d_sum, dst=0)
-            dist.reduce(d_n, dst=0)
-            dist.reduce(d_m, dst=0)
+        merge_accumulators([d_sum, d_n, d_m], dist)  # one RCCL reduce per accumulator plane
         if rank == 0:
             f_sum.add_(d_sum)
             f_n.add_(d_n)

@@ -79,11 +79,15 @@ class rt_scene_info(C.Structure):
 _lib: Optional[C.CDLL] = None
 
 
-def load_library(path: str = LIB_PATH) -> C.CDLL:
-    """Load librtcore_hip.so (built by __graft_entry__.build()).  Raises if it is missing."""
+def load_library(path: str = "") -> C.CDLL:
+    """Load librtcore_hip.so (built by __graft_entry__.build()).  Raises if it is missing.
+
+    RTCORE_LIB may name an alternative build of the same library (e.g. a tuning variant).
+    """
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("RTCORE_LIB", "") or LIB_PATH
     if not os.path.exists(path):
         raise RtError(f"{path} is missing: run __graft_entry__.build() (make -C raytracercore_amd/csrc)")
     # torch-ROCm wheels carry their own HIP runtime; when torch is present it must be loaded

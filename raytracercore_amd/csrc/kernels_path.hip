@@ -18,6 +18,10 @@
 // Util.RayHitMatches' self-hit rejection (Util.cs:179-192) restated as: a flat primitive
 // is never re-hit by the ray leaving it; a sphere re-hit keeps only the far root when the
 // ray heads into it (DESIGN.md §Self-hit rule).
+//
+// Brute-force traversal walks the primitive records with a wave-uniform index: the records
+// come through the scalar data cache (s_load) into SGPRs and every lane tests every
+// primitive branch-free.  BVH traversal keeps a per-lane stack in LDS.
 #include "../../include/rtcore_rng.h"
 #include "rt_kernels.h"
 
@@ -35,135 +39,115 @@ __device__ __forceinline__ V3 operator*(V3 a, float s) { return {a.x * s, a.y * 
 __device__ __forceinline__ V3 operator*(V3 a, V3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
 __device__ __forceinline__ V3 operator-(V3 a) { return {-a.x, -a.y, -a.z}; }
 __device__ __forceinline__ float dot(V3 a, V3 b) { return fmaf(a.x, b.x, fmaf(a.y, b.y, a.z * b.z)); }
+__device__ __forceinline__ float dot4(float4 r, V3 p) { return fmaf(r.x, p.x, fmaf(r.y, p.y, fmaf(r.z, p.z, r.w))); }
+__device__ __forceinline__ float dot3(float4 r, V3 p) { return fmaf(r.x, p.x, fmaf(r.y, p.y, r.z * p.z)); }
 __device__ __forceinline__ V3 cross(V3 a, V3 b)
 {
     return {fmaf(a.y, b.z, -a.z * b.y), fmaf(a.z, b.x, -a.x * b.z), fmaf(a.x, b.y, -a.y * b.x)};
 }
 __device__ __forceinline__ V3 madd(V3 a, float s, V3 c) { return {fmaf(a.x, s, c.x), fmaf(a.y, s, c.y), fmaf(a.z, s, c.z)}; }
-__device__ __forceinline__ V3 normalize(V3 a)
-{
-    float r = __builtin_amdgcn_rsqf(dot(a, a));
-    return a * r;
-}
 __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
-__device__ __forceinline__ V3 xf_point(const float4* m, V3 p)
-{
-    return {fmaf(m[0].x, p.x, fmaf(m[0].y, p.y, fmaf(m[0].z, p.z, m[0].w))),
-            fmaf(m[1].x, p.x, fmaf(m[1].y, p.y, fmaf(m[1].z, p.z, m[1].w))),
-            fmaf(m[2].x, p.x, fmaf(m[2].y, p.y, fmaf(m[2].z, p.z, m[2].w)))};
-}
-__device__ __forceinline__ V3 xf_dir(const float4* m, V3 p)
-{
-    return {fmaf(m[0].x, p.x, fmaf(m[0].y, p.y, m[0].z * p.z)), fmaf(m[1].x, p.x, fmaf(m[1].y, p.y, m[1].z * p.z)),
-            fmaf(m[2].x, p.x, fmaf(m[2].y, p.y, m[2].z * p.z))};
-}
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ V3 normalize(V3 a) { return a * __builtin_amdgcn_rsqf(dot(a, a)); }
+__device__ __forceinline__ V3 xf_point(const float4* m, V3 p) { return {dot4(m[0], p), dot4(m[1], p), dot4(m[2], p)}; }
+__device__ __forceinline__ V3 xf_dir(const float4* m, V3 p) { return {dot3(m[0], p), dot3(m[1], p), dot3(m[2], p)}; }
 
 struct Best {
     float t;    // world distance (Hit.Distance)
-    int slot;   // index into the primitive array of the traversal mode, -1 = none
-    float u, v; // triangle barycentrics | sphere: object-space ray parameter in u
+    int slot;   // primitive slot of the traversal mode, -1 = none
+    float u, v; // triangle barycentrics | sphere: object-space ray parameter in u | plane: t in u
     int gin;    // geometric inside before Invert (selects the flipped normal)
 };
 
-__device__ __forceinline__ void test_tri(const PrimF& P, int slot, V3 o, V3 d, int prev, Best& b)
+// Triangle via the affine inverse record (TestRec): w(t) = 0 gives t, then (u, v).
+// Inside (Moller-Trumbore's 1/det < 0, Triangle.cs:127) <=> d . n > 0 <=> dw > 0.
+__device__ __forceinline__ void hit_tri(const TestRec& R, int slot, V3 o, V3 d, int prev, Best& b)
 {
-    const int id = __float_as_int(P.a.w);
-    if (id == prev) return; // a flat primitive cannot be re-hit after leaving it
-    const uint32_t fl = __float_as_uint(P.b.w);
-    const V3 off = o - xyz(P.a);
-    const V3 e1 = xyz(P.b), e2 = xyz(P.c);
-    const V3 s1 = cross(off, e1);
-    const V3 s2 = cross(d, e2);
-    const float inv = rcp(dot(e1, s2));
-    const float t = dot(e2, s1) * inv;
-    if (!(t >= 0.0f && t < b.t)) return;
-    const float u = dot(off, s2) * inv, v = dot(d, s1) * inv;
-    const bool rej = (u < 0.0f) | (v < 0.0f) | ((fl & F_MIRROR) ? ((u > 1.0f) | (v > 1.0f)) : (u + v > 1.0f));
-    if (rej) return;
-    const int gin = inv < 0.0f;
-    const bool ins = gin ^ ((fl & F_INVERT) != 0);
-    if (ins && !(fl & F_TWOSIDED)) return;
-    b = Best{t, slot, u, v, gin};
+    const int id = __float_as_int(R.meta.x);
+    const uint32_t fl = __float_as_uint(R.meta.y);
+    const float dw = dot3(R.r2, d);
+    const float t = -dot4(R.r2, o) * rcp(dw);
+    const float u = fmaf(t, dot3(R.r0, d), dot4(R.r0, o));
+    const float v = fmaf(t, dot3(R.r1, d), dot4(R.r1, o));
+    const bool gin = dw > 0.0f;
+    bool ok = (t >= 0.0f) & (t < b.t) & (u >= 0.0f) & (v >= 0.0f) & (id != prev);
+    ok &= (fl & F_MIRROR) ? ((u <= 1.0f) & (v <= 1.0f)) : (u + v <= 1.0f);
+    if (!(fl & F_TWOSIDED)) ok &= !(gin ^ ((fl & F_INVERT) != 0)); // one-sided: cull Inside
+    b.t = ok ? t : b.t;
+    b.slot = ok ? slot : b.slot;
+    b.u = ok ? u : b.u;
+    b.v = ok ? v : b.v;
+    b.gin = ok ? (int)gin : b.gin;
 }
 
-__device__ __forceinline__ void test_sph(const PrimF& P, int slot, V3 o, V3 d, int prev, const XformF* xf, Best& b)
+// Sphere (Sphere.cs:50-155).  Primitive.RayTrace returns the first surviving root: the close
+// one (Inside = false) if it lies ahead and is not culled, otherwise the far one.
+__device__ __forceinline__ void hit_sph(const TestRec& R, int slot, V3 o, V3 d, int prev, const XformF* __restrict__ xf,
+                                        Best& b)
 {
-    const int id = __float_as_int(P.a.w);
-    const uint32_t fl = __float_as_uint(P.b.w);
+    const int id = __float_as_int(R.meta.x);
+    const uint32_t fl = __float_as_uint(R.meta.y);
     V3 oo = o, dd = d;
     float k = 1.0f; // object-space ray parameter -> world distance
     if (fl & F_TRANSFORMED) {
-        const XformF& X = xf[__float_as_int(P.b.z)];
+        const XformF& X = xf[__float_as_int(R.r1.y)];
         oo = xf_point(X.to_world, o);
-        V3 dl = xf_dir(X.to_world, d);
-        float il = __builtin_amdgcn_rsqf(dot(dl, dl));
-        dd = dl * il;
-        k = il; // |to_obj * dd| = 1 / |to_world * d|
+        const V3 dl = xf_dir(X.to_world, d);
+        k = __builtin_amdgcn_rsqf(dot(dl, dl)); // |to_obj * dd| = 1 / |to_world * d|
+        dd = dl * k;
     }
-    const V3 oc = oo - xyz(P.a);
+    const V3 oc = oo - xyz(R.r0);
     const float bb = dot(oc, dd);
-    float tn = -1.0f, tf;
-    if (id == prev) {
-        // the root at the bounce point is the skipped self-hit; the other root is -2 (oc.dd)
-        if (!(bb < 0.0f)) return;
-        tf = -2.0f * bb;
-    } else {
-        const V3 l = madd(dd, -bb, oc);
-        const float disc = P.b.y - dot(l, l);
-        if (!(disc >= 0.0f)) return;
-        const float sq = sqrtf(disc);
-        tn = -bb - sq;
-        tf = -bb + sq;
-        if (!(tf >= 0.0f)) return;
-    }
-    const bool inv = (fl & F_INVERT) != 0, two = (fl & F_TWOSIDED) != 0;
-    if (tn >= 0.0f && (two || !inv)) { // close hit: Inside = false (^ Invert)
-        const float tw = tn * k;
-        if (tw < b.t) b = Best{tw, slot, tn, 0.0f, 0};
-        return;
-    }
-    if (two || inv) { // far hit: Inside = true (^ Invert)
-        const float tw = tf * k;
-        if (tw < b.t) b = Best{tw, slot, tf, 0.0f, 1};
-    }
+    const V3 l = madd(dd, -bb, oc);
+    const float disc = R.r1.x - dot(l, l);
+    const float sq = fsqrt(fmaxf(disc, 0.0f));
+    const bool self = id == prev;
+    // self-hit: the root at the bounce point is skipped; the other root is -2 (oc.dd)
+    const float tn = self ? -1.0f : -bb - sq;
+    const float tf = self ? -2.0f * bb : sq - bb;
+    const bool any = self ? (bb < 0.0f) : ((disc >= 0.0f) & (tf >= 0.0f));
+    const bool two = (fl & F_TWOSIDED) != 0, inv = (fl & F_INVERT) != 0;
+    const bool use_close = any & (tn >= 0.0f) & (two | !inv);
+    const bool use_far = !use_close & any & (two | inv);
+    const float tc = use_close ? tn : tf;
+    const float tw = tc * k;
+    const bool ok = (use_close | use_far) & (tw < b.t);
+    b.t = ok ? tw : b.t;
+    b.slot = ok ? slot : b.slot;
+    b.u = ok ? tc : b.u;
+    b.gin = ok ? (int)use_far : b.gin;
 }
 
-__device__ __forceinline__ void test_plane(const PrimF& P, int slot, V3 o, V3 d, int prev, Best& b)
+// Plane (Plane.cs:36-66), including the NearlyEqual branch for rays in the plane.
+__device__ __forceinline__ void hit_plane(const TestRec& R, int slot, V3 o, V3 d, int prev, Best& b)
 {
-    const int id = __float_as_int(P.a.w);
-    if (id == prev) return;
-    const uint32_t fl = __float_as_uint(P.b.w);
-    const V3 n = xyz(P.a);
-    const float pd = P.b.x;
+    const int id = __float_as_int(R.meta.x);
+    const uint32_t fl = __float_as_uint(R.meta.y);
+    const V3 n = xyz(R.r0);
+    const float pd = R.r0.w;
     const float rd = dot(o, n), den = dot(d, n);
-    float dist;
-    int gin;
-    if (den == 0.0f) {
-        // Plane.DoRayTrace's NearlyEqual branch (Plane.cs:41-45, Util.cs:41-51)
-        if (!(pd == rd || fmaxf(pd, rd) < 0.0f)) return;
-        dist = 0.0f;
-        gin = 1;
-    } else {
-        const float t = (pd - rd) / den;
-        if (!(t >= -1e-24f)) return;
-        dist = fabsf(t);
-        gin = dot(n, d) > 0.0f;
-    }
-    const bool ins = gin ^ ((fl & F_INVERT) != 0);
-    if (ins && !(fl & F_TWOSIDED)) return;
-    if (dist < b.t) b = Best{dist, slot, dist, 0.0f, gin};
+    const float t = (pd - rd) / den;
+    const bool flat = den == 0.0f;
+    const bool any = flat ? ((pd == rd) | (fmaxf(pd, rd) < 0.0f)) : (t >= -1e-24f);
+    const float dist = flat ? 0.0f : fabsf(t);
+    const bool gin = flat ? true : (den > 0.0f);
+    bool ok = any & (id != prev) & (dist < b.t);
+    if (!(fl & F_TWOSIDED)) ok &= !(gin ^ ((fl & F_INVERT) != 0));
+    b.t = ok ? dist : b.t;
+    b.slot = ok ? slot : b.slot;
+    b.u = ok ? (flat ? 0.0f : t) : b.u;
+    b.gin = ok ? (int)gin : b.gin;
 }
 
-// Closest hit over every primitive; the loop index is wave-uniform, so the primitive
-// records stream through the scalar data cache.
-__device__ __forceinline__ void trace_brute(const DevScene& s, V3 o, V3 d, int prev, Best& b, unsigned long long* st)
+__device__ __forceinline__ void hit_any(const TestRec& R, int slot, V3 o, V3 d, int prev, const XformF* __restrict__ xf,
+                                        Best& b)
 {
-    const PrimF* __restrict__ P = s.prims_bf;
-    int i = 0;
-    for (; i < s.n_tri; i++) test_tri(P[i], i, o, d, prev, b);
-    for (; i < s.n_tri + s.n_sph; i++) test_sph(P[i], i, o, d, prev, s.xf, b);
+    switch (__float_as_uint(R.meta.y) & KIND_MASK) {
+    case RT_PRIM_TRIANGLE: hit_tri(R, slot, o, d, prev, b); break;
+    case RT_PRIM_SPHERE: hit_sph(R, slot, o, d, prev, xf, b); break;
+    default: hit_plane(R, slot, o, d, prev, b); break;
+    }
 }
-
 
 __device__ __forceinline__ bool slab(float4 lo, float4 hi, V3 oi, V3 id, float tmax, float& tnear)
 {
@@ -177,9 +161,14 @@ __device__ __forceinline__ bool slab(float4 lo, float4 hi, V3 oi, V3 id, float t
     return tmin <= tmx * 1.00000024f;
 }
 
-template <int STACK>
-__device__ __forceinline__ void trace_bvh(const DevScene& s, V3 o, V3 d, int prev, Best& b, int* stk,
-                                          unsigned long long* st)
+struct Counters {
+    unsigned nodes, tris, sphs;
+};
+
+template <int STACK, bool STATS>
+__device__ __forceinline__ void trace_bvh(const PathScene& s, const NodeF* __restrict__ nodes,
+                                          const TestRec* __restrict__ tests, const XformF* __restrict__ xf, V3 o, V3 d,
+                                          int prev, Best& b, int* stk, Counters& cnt)
 {
     const V3 id = v3(rcp(d.x), rcp(d.y), rcp(d.z));
     const V3 oi = o * id;
@@ -187,7 +176,8 @@ __device__ __forceinline__ void trace_bvh(const DevScene& s, V3 o, V3 d, int pre
     int sp = 0;
     while (true) {
         if (ref >= 0) {
-            const NodeF n = s.nodes[ref];
+            const NodeF n = nodes[ref];
+            if (STATS) cnt.nodes++;
             float tl, tr;
             const bool hl = slab(n.lmin, n.lmax, oi, id, b.t, tl);
             const bool hr = slab(n.rmin, n.rmax, oi, id, b.t, tr);
@@ -198,17 +188,24 @@ __device__ __forceinline__ void trace_bvh(const DevScene& s, V3 o, V3 d, int pre
                 ref = lf ? cl : cr;
                 continue;
             }
-            if (hl) { ref = cl; continue; }
-            if (hr) { ref = cr; continue; }
+            if (hl) {
+                ref = cl;
+                continue;
+            }
+            if (hr) {
+                ref = cr;
+                continue;
+            }
         } else {
             const int code = ~ref;
-            const int first = code >> 3, cnt = (code & 7) + 1;
-            for (int k = first; k < first + cnt; k++) {
-                const PrimF P = s.prims_bvh[k];
-                if ((__float_as_uint(P.b.w) & KIND_MASK) == RT_PRIM_TRIANGLE)
-                    test_tri(P, k, o, d, prev, b);
-                else
-                    test_sph(P, k, o, d, prev, s.xf, b);
+            const int first = code >> 3, c = (code & 7) + 1;
+            for (int k = first; k < first + c; k++) {
+                const TestRec R = tests[k];
+                if (STATS) {
+                    if ((__float_as_uint(R.meta.y) & KIND_MASK) == RT_PRIM_TRIANGLE) cnt.tris++;
+                    else cnt.sphs++;
+                }
+                hit_any(R, k, o, d, prev, xf, b);
             }
         }
         if (sp == 0) break;
@@ -230,7 +227,7 @@ __device__ __forceinline__ float next_u(rt_rng& r) { return rt_rng_next_float(&r
 __device__ __forceinline__ V3 horizon(V3 pole, float z, float s, float turn)
 {
     V3 c = v3(pole.y, -pole.x, 0.0f);
-    const float cl = c.x * c.x + c.y * c.y;
+    const float cl = fmaf(c.x, c.x, c.y * c.y);
     c = (cl == 0.0f) ? v3(1.0f, 0.0f, 0.0f) : c * __builtin_amdgcn_rsqf(cl);
     const V3 bn = cross(pole, c);
     const float cs = __builtin_amdgcn_cosf(turn), sn = __builtin_amdgcn_sinf(turn); // argument in turns
@@ -241,8 +238,8 @@ __device__ __forceinline__ V3 horizon(V3 pole, float z, float s, float turn)
 __device__ __forceinline__ void camera_ray(const CameraF& c, float x, float y, V3& o, V3& d)
 {
     if (c.kind == RT_CAMERA_FRUSTUM) {
-        const float ox = c.tan_x * ((x - c.w2) / c.w2);
-        const float oy = c.tan_y * ((y - c.h2) / c.h2);
+        const float ox = c.tan_x * ((x - c.w2) * rcp(c.w2));
+        const float oy = c.tan_y * ((y - c.h2) * rcp(c.h2));
         d = normalize(madd(xyz(c.up), oy, madd(xyz(c.side), ox, xyz(c.look))));
         o = xyz(c.position);
     } else {
@@ -260,7 +257,7 @@ __device__ __forceinline__ void start_sample(const CameraF& cam, int x, int y, S
     camera_ray(cam, sx, sy, S.o, S.d);
     if (cam.dof != 0.0f) {
         const V3 focus = madd(S.d, cam.focal_length - cam.image_plane, S.o);
-        const float dist = sqrtf(next_u(S.rng)) * cam.dof;
+        const float dist = fsqrt(next_u(S.rng)) * cam.dof;
         const float turn = next_u(S.rng);
         const float ox = __builtin_amdgcn_cosf(turn) * dist, oy = __builtin_amdgcn_sinf(turn) * dist;
         V3 o2, d2;
@@ -273,19 +270,29 @@ __device__ __forceinline__ void start_sample(const CameraF& cam, int x, int y, S
     S.prev = -1;
 }
 
+// 1 - z^2 for z = 2^a (a <= 0) without cancellation: 1 - 2^(2a) = -expm1(2a ln 2)
+__device__ __forceinline__ float one_minus_exp2_2a(float a)
+{
+    const float x = 2.0f * a * 0.69314718055994531f;
+    if (x > -0.0625f) return -x * fmaf(x, fmaf(x, fmaf(x, 1.0f / 24.0f, 1.0f / 6.0f), 0.5f), 1.0f);
+    return 1.0f - __builtin_amdgcn_exp2f(2.0f * a);
+}
+
 // One bounce of Raytracer.GetColor after the closest-hit query.  Returns 0 to continue the
 // path, 1 if the sample ended with colour `col`, 2 if it ended as a miss (Placeholder).
-__device__ __forceinline__ int shade(const DevScene& s, const PrimF* prims, const Best& b, Sample& S, V3& col)
+__device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict__ prims, const MatF* __restrict__ mats,
+                                     const XformF* __restrict__ xfs, const float4* __restrict__ vnormals, const Best& b,
+                                     Sample& S, V3& col)
 {
     if (b.slot < 0) {
         if (S.bounce == 0 || s.ambient_miss) return 2;
-        col = v3(s.ambient.x, s.ambient.y, s.ambient.z);
+        col = v3(s.ambient_r, s.ambient_g, s.ambient_b);
         return 1;
     }
     const PrimF P = prims[b.slot];
     const uint32_t fl = __float_as_uint(P.b.w);
     const int id = __float_as_int(P.a.w);
-    const MatF& M = s.mats[id];
+    const MatF& M = mats[id];
     const uint32_t kind = fl & KIND_MASK;
     const V3 emis = xyz(M.emission);
     if (s.debug_geom) { // Raytracer.cs:93-98
@@ -301,7 +308,7 @@ __device__ __forceinline__ int shade(const DevScene& s, const PrimF* prims, cons
     if (kind == RT_PRIM_TRIANGLE) {
         pos = madd(xyz(P.b), b.u, madd(xyz(P.c), b.v, xyz(P.a)));
         if (fl & F_HASNORMALS) { // Triangle.GetNormal quirk: Normal is never set -> NaN when inside
-            const float4* vn = s.vnormals + 3 * id;
+            const float4* vn = vnormals + 3 * id;
             nrm = normalize(madd(xyz(vn[2]), b.u + b.v, madd(xyz(vn[1]), b.v, xyz(vn[0]) * b.u)));
             if (b.gin) nrm = v3(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
         } else {
@@ -310,7 +317,7 @@ __device__ __forceinline__ int shade(const DevScene& s, const PrimF* prims, cons
     } else if (kind == RT_PRIM_SPHERE) {
         V3 oo = S.o, dd = S.d;
         const bool tr = (fl & F_TRANSFORMED) != 0;
-        const XformF* X = tr ? &s.xf[__float_as_int(P.b.z)] : nullptr;
+        const XformF* X = tr ? &xfs[__float_as_int(P.b.z)] : nullptr;
         if (tr) {
             oo = xf_point(X->to_world, S.o);
             dd = normalize(xf_dir(X->to_world, S.d));
@@ -334,9 +341,9 @@ __device__ __forceinline__ int shade(const DevScene& s, const PrimF* prims, cons
     const float shin = M.shininess;
     float z = 1.0f, sz = 0.0f;
     if (!(__builtin_isinf(shin) && shin > 0.0f)) {
-        const float a = __builtin_amdgcn_logf(next_u(S.rng)) / shin; // log2
+        const float a = __builtin_amdgcn_logf(next_u(S.rng)) * rcp(shin); // log2(U) / shininess
         z = __builtin_amdgcn_exp2f(a);
-        sz = sqrtf(-expm1f(2.0f * a * 0.69314718055994531f)); // sqrt(1 - z^2) without cancellation
+        sz = fsqrt(one_minus_exp2_2a(a));
     }
     const V3 rough = horizon(nrm, z, sz, next_u(S.rng));
 
@@ -347,14 +354,14 @@ __device__ __forceinline__ int shade(const DevScene& s, const PrimF* prims, cons
     if (((refr_lum > 0.0f) | (spec_lum > 0.0f)) && M.ior != 0.0f && cs >= 0.0f) { // Raytracer.cs:120-161
         const float ior_in = inside ? M.ior : s.air_ior;
         const float ior_out = inside ? s.air_ior : M.ior;
-        ior_ratio = ior_in / ior_out;
-        const float sin_out = ior_ratio * sqrtf(1.0f - cs * cs);
+        ior_ratio = ior_in * rcp(ior_out);
+        const float sin_out = ior_ratio * fsqrt(1.0f - cs * cs);
         if (sin_out >= 1.0f) {
             refr_lum = 0.0f;
         } else {
-            cos_out = sqrtf(1.0f - sin_out * sin_out);
-            const float rs = (ior_out * cs - ior_in * cos_out) / (ior_out * cs + ior_in * cos_out);
-            const float rp = (ior_in * cs - ior_out * cos_out) / (ior_in * cs + ior_out * cos_out);
+            cos_out = fsqrt(1.0f - sin_out * sin_out);
+            const float rs = (ior_out * cs - ior_in * cos_out) * rcp(ior_out * cs + ior_in * cos_out);
+            const float rp = (ior_in * cs - ior_out * cos_out) * rcp(ior_in * cs + ior_out * cos_out);
             const float ratio = (rs * rs + rp * rp) * 0.5f;
             spec_lum *= ratio;
             refr_lum *= 1.0f - ratio;
@@ -382,7 +389,7 @@ __device__ __forceinline__ int shade(const DevScene& s, const PrimF* prims, cons
         new_tint = xyz(M.specular);
     } else if (diff_lum != 0.0f && (ray_rand -= diff_lum) <= 0.0f) { // diffuse
         const float dz = 2.0f * acosf(next_u(S.rng)) * 0.31830988618379067f;
-        const float ds = sqrtf(fmaxf(0.0f, 1.0f - dz * dz));
+        const float ds = fsqrt(fmaxf(0.0f, 1.0f - dz * dz));
         out_dir = horizon(nrm, dz, ds, next_u(S.rng));
         new_tint = xyz(M.diffuse);
     } else { // emission
@@ -398,20 +405,27 @@ __device__ __forceinline__ int shade(const DevScene& s, const PrimF* prims, cons
 }
 
 // TRAV: RT_TRAVERSAL_BRUTE, or RT_TRAVERSAL_BVH with an LDS stack of STACK entries per lane.
+#ifndef RT_PATH_WAVES
+#define RT_PATH_WAVES 4 // minimum waves per SIMD the register allocator must allow
+#endif
 template <int TRAV, int STACK, bool STATS>
-__global__ void __launch_bounds__(256) path_kernel(DevScene s, CameraF cam, PathParams p)
+__global__ void __launch_bounds__(256, RT_PATH_WAVES)
+    path_kernel(PathScene s, CameraF cam, PathParams p, const TestRec* __restrict__ tests,
+                const PrimF* __restrict__ prims, const NodeF* __restrict__ nodes, const XformF* __restrict__ xf,
+                const MatF* __restrict__ mats, const float4* __restrict__ vnormals)
 {
     __shared__ int stack_mem[TRAV == RT_TRAVERSAL_BVH ? STACK * 256 : 1];
     int* stk = stack_mem + threadIdx.x;
     const int lane = threadIdx.x & 63;
     const unsigned total = (unsigned)p.n_chunks * (unsigned)p.n_pad;
-    const PrimF* prims = TRAV == RT_TRAVERSAL_BVH ? s.prims_bvh : s.prims_bf;
+    const int pln0 = s.n_tri + s.n_sph;
 
     bool active = true, item_open = false, live = false;
     unsigned item = 0;
     int px = 0, py = 0, s_next = 0, s_end = 0;
     float ar = 0.0f, ag = 0.0f, ab = 0.0f;
     unsigned n_s = 0, n_m = 0, rays = 0;
+    Counters cnt{0, 0, 0};
     Sample S;
     S.prev = -1;
     S.bounce = 0;
@@ -461,17 +475,19 @@ __global__ void __launch_bounds__(256) path_kernel(DevScene s, CameraF cam, Path
         if (live) {
             Best b{__builtin_huge_valf(), -1, 0.0f, 0.0f, 0};
             if (TRAV == RT_TRAVERSAL_BVH) {
-                trace_bvh<STACK>(s, S.o, S.d, S.prev, b, stk, STATS ? p.stats : nullptr);
+                trace_bvh<STACK, STATS>(s, nodes, tests, xf, S.o, S.d, S.prev, b, stk, cnt);
             } else {
-                trace_brute(s, S.o, S.d, S.prev, b, STATS ? p.stats : nullptr);
+                for (int i = 0; i < s.n_tri; i++) hit_tri(tests[i], i, S.o, S.d, S.prev, b);
+                for (int i = s.n_tri; i < pln0; i++) hit_sph(tests[i], i, S.o, S.d, S.prev, xf, b);
+                if (STATS) {
+                    cnt.tris += s.n_tri;
+                    cnt.sphs += s.n_sph;
+                }
             }
-            for (int i = 0; i < s.n_pln; i++) test_plane(s.prims_bf[s.n_tri + s.n_sph + i], s.n_tri + s.n_sph + i, S.o,
-                                                       S.d, S.prev, b);
+            for (int i = pln0; i < pln0 + s.n_pln; i++) hit_plane(tests[i], i, S.o, S.d, S.prev, b);
             rays++;
             V3 col;
-            // planes live in the brute-force array in both modes
-            const bool plane_hit = b.slot >= s.n_tri + s.n_sph && TRAV == RT_TRAVERSAL_BVH;
-            const int r = plane_hit ? shade(s, s.prims_bf, b, S, col) : shade(s, prims, b, S, col);
+            const int r = shade(s, prims, mats, xf, vnormals, b, S, col);
             if (r != 0) {
                 if (r == 1) {
                     ar += col.x;
@@ -486,10 +502,23 @@ __global__ void __launch_bounds__(256) path_kernel(DevScene s, CameraF cam, Path
             }
         }
     }
-    // one 64-bit add per wave for the ray count
+    // one 64-bit add per wave for the ray count (and the optional traversal counters)
     unsigned long long wr = rays;
     for (int off = 32; off > 0; off >>= 1) wr += __shfl_down(wr, off);
     if (lane == 0) atomicAdd(p.rays, wr);
+    if (STATS) {
+        unsigned long long a = cnt.nodes, t = cnt.tris, q = cnt.sphs;
+        for (int off = 32; off > 0; off >>= 1) {
+            a += __shfl_down(a, off);
+            t += __shfl_down(t, off);
+            q += __shfl_down(q, off);
+        }
+        if (lane == 0) {
+            atomicAdd(p.stats + 0, a);
+            atomicAdd(p.stats + 1, t);
+            atomicAdd(p.stats + 2, q);
+        }
+    }
 }
 
 __global__ void accumulate_kernel(PathParams p, double* sum, uint32_t* samples, uint32_t* misses)
@@ -531,9 +560,10 @@ __global__ void colors_1spp_kernel(PathParams p, double* out)
     out[o + 2] = miss ? -1.0 : (double)v.z;
 }
 
-using PathKernel = void (*)(DevScene, CameraF, PathParams);
+using PathKernel = void (*)(PathScene, CameraF, PathParams, const TestRec*, const PrimF*, const NodeF*,
+                            const XformF*, const MatF*, const float4*);
 
-// traversal: 0 brute force, 1 BVH with a 24-entry stack, 2 BVH with a 48-entry stack
+// variant: 0 brute force, 1 BVH with a 24-entry stack, 2 BVH with a 48-entry stack
 PathKernel pick(int variant, bool stats)
 {
     switch (variant) {
@@ -564,10 +594,30 @@ int path_blocks_per_cu(int variant, bool stats)
 hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& p, int variant, int grid_blocks,
                        hipStream_t stream, bool stats)
 {
-    DevScene sa = s;
+    PathScene ps;
+    ps.n_tri = s.n_tri;
+    ps.n_sph = s.n_sph;
+    ps.n_pln = s.n_pln;
+    ps.n_bvh = s.n_tri + s.n_sph;
+    ps.root = s.root;
+    ps.width = s.width;
+    ps.recursion = s.recursion;
+    ps.debug_geom = s.debug_geom;
+    ps.ambient_miss = s.ambient_miss;
+    ps.air_ior = s.air_ior;
+    ps.ambient_r = s.ambient.x;
+    ps.ambient_g = s.ambient.y;
+    ps.ambient_b = s.ambient.z;
     CameraF ca = cam;
     PathParams pa = p;
-    void* args[] = {&sa, &ca, &pa};
+    const bool bvh = variant != 0;
+    const TestRec* tests = bvh ? s.tests_bvh : s.tests_bf;
+    const PrimF* prims = bvh ? s.prims_bvh : s.prims_bf;
+    const NodeF* nodes = s.nodes;
+    const XformF* xf = s.xf;
+    const MatF* mats = s.mats;
+    const float4* vn = s.vnormals;
+    void* args[] = {&ps, &ca, &pa, &tests, &prims, &nodes, &xf, &mats, &vn};
     return hipLaunchKernel(reinterpret_cast<const void*>(pick(variant, stats)), dim3(grid_blocks), dim3(256), args, 0,
                            stream);
 }

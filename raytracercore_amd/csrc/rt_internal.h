@@ -77,6 +77,31 @@ struct alignas(16) MatF {       // per primitive ID, 80 B
     float pad;
 };
 
+// Intersection record of the fp32 kernel (64 B), one per primitive slot:
+//   triangle: rows r0..r2 of the affine inverse of [e01 e02 n | v0], so that
+//             (u, v, w) = M (p, 1): w = 0 on the plane, (u, v) = the barycentrics the
+//             reference's Moller-Trumbore test computes (Triangle.cs:77-146)
+//   sphere:   r0 = (centre, radius), r1 = (radius^2, bitcast xf index, 0, 0)
+//   plane:    r0 = (normal, origin distance)
+//   meta = (bitcast primitive ID, bitcast flags, 0, 0)
+struct alignas(16) TestRec {
+    float4 r0, r1, r2, meta;
+};
+
+// Scalar fields of the path kernel (pointers are passed as separate __restrict__ arguments
+// so that the wave-uniform primitive loop is served by scalar loads).
+struct PathScene {
+    int32_t n_tri, n_sph, n_pln; // brute-force order: triangles | spheres | planes
+    int32_t n_bvh;               // primitives in the BVH (all but planes); planes follow them
+    int32_t root;                // child reference of the BVH root
+    int32_t width;               // frame width (RNG pixel index)
+    int32_t recursion;
+    int32_t debug_geom;
+    int32_t ambient_miss;
+    float air_ior;
+    float ambient_r, ambient_g, ambient_b;
+};
+
 // Child reference in a NodeF: >= 0 internal node index, < 0 leaf = ~(first << 3 | (count-1)).
 struct alignas(16) NodeF {      // 64 B: both children's boxes
     float4 lmin; // xyz, w = bitcast int left child
@@ -98,12 +123,15 @@ struct CameraD {                // post-InitRender state in fp64 (exact kernel)
     int32_t pad;
 };
 
-// Everything a kernel needs, passed by value.
+// Everything the kernels need (device pointers + scene fields).
 struct DevScene {
-    // fast set
-    const PrimF* prims_bf;      // brute-force order: triangles | spheres | planes
+    // fast set; slot order is [triangles | spheres | planes] for brute force and
+    // [BVH leaf order | planes] for the BVH, with matching TestRec / PrimF arrays
+    const TestRec* tests_bf;
+    const PrimF* prims_bf;
     int32_t n_tri, n_sph, n_pln;
-    const PrimF* prims_bvh;     // BVH leaf order (planes excluded: always brute force)
+    const TestRec* tests_bvh;
+    const PrimF* prims_bvh;
     const NodeF* nodes;
     int32_t n_nodes;
     int32_t root;               // child reference of the root (may be a leaf)

@@ -90,6 +90,7 @@ struct rt_scene {
     SahBvh sah;
     DevScene dev{};
     DevBuf<PrimF> prims_bf, prims_bvh;
+    DevBuf<TestRec> tests_bf, tests_bvh;
     DevBuf<NodeF> nodes;
     DevBuf<XformF> xf;
     DevBuf<MatF> mats;
@@ -192,16 +193,49 @@ int upload_scene(rt_scene* s)
         }
         return f;
     };
-    std::vector<PrimF> bf;
+    auto testrec = [&](int i) {
+        const HostPrim& p = H[i];
+        TestRec t;
+        std::memset(&t, 0, sizeof t);
+        t.meta = make_float4(as_f(i), as_f(p.flags), 0.0f, 0.0f);
+        if (p.kind == RT_PRIM_TRIANGLE) {
+            // inverse of A = [e01 e02 n] (columns) with n = e01 x e02: rows (e02 x n, n x e01, n) / |n|^2
+            const Vec4d e1 = p.e01, e2 = p.e02, nn = cross_s(p.e01, p.e02);
+            const double D = dot_s(e1, cross_s(e2, nn));
+            const Vec4d rows[3] = {cross_s(e2, nn), cross_s(nn, e1), nn};
+            float4* out[3] = {&t.r0, &t.r1, &t.r2};
+            for (int k = 0; k < 3; k++) {
+                const Vec4d r = divs(rows[k], D);
+                *out[k] = make_float4((float)r.x, (float)r.y, (float)r.z,
+                                      (float)(-(r.x * p.v[0].x + r.y * p.v[0].y + r.z * p.v[0].z)));
+            }
+        } else if (p.kind == RT_PRIM_SPHERE) {
+            t.r0 = f4(p.center, (float)p.radius);
+            t.r1 = make_float4((float)p.radius_sqr, as_f(xf_index[i]), 0.0f, 0.0f);
+        } else {
+            t.r0 = f4(p.pn, (float)p.pd);
+        }
+        return t;
+    };
+    std::vector<PrimF> bf, bv;
+    std::vector<TestRec> tbf, tbv;
     int nt = 0, ns = 0, np = 0;
     for (int kind = 0; kind < 3; kind++)
         for (int i = 0; i < n; i++)
             if (H[i].kind == kind) {
                 bf.push_back(primf(i));
+                tbf.push_back(testrec(i));
                 (kind == 0 ? nt : kind == 1 ? ns : np)++;
             }
-    std::vector<PrimF> bv;
-    for (int i : s->sah.order) bv.push_back(primf(i));
+    for (int i : s->sah.order) {
+        bv.push_back(primf(i));
+        tbv.push_back(testrec(i));
+    }
+    for (int i = 0; i < n; i++) // planes follow the BVH's primitives in both orders
+        if (H[i].kind == RT_PRIM_PLANE) {
+            bv.push_back(primf(i));
+            tbv.push_back(testrec(i));
+        }
     std::vector<MatF> mats(n);
     for (int i = 0; i < n; i++) {
         const HostPrim& p = H[i];
@@ -223,6 +257,8 @@ int upload_scene(rt_scene* s)
     HIP_TRY(s->ref_nodes.upload(s->ref.nodes));
     HIP_TRY(s->prims_bf.upload(bf));
     HIP_TRY(s->prims_bvh.upload(bv));
+    HIP_TRY(s->tests_bf.upload(tbf));
+    HIP_TRY(s->tests_bvh.upload(tbv));
     HIP_TRY(s->nodes.upload(s->sah.nodes));
     HIP_TRY(s->xf.upload(xf));
     HIP_TRY(s->mats.upload(mats));
@@ -232,6 +268,8 @@ int upload_scene(rt_scene* s)
                       xf.size() * sizeof(XformF) + mats.size() * sizeof(MatF) + vn.size() * sizeof(float4);
 
     DevScene& d = s->dev;
+    d.tests_bf = s->tests_bf.p;
+    d.tests_bvh = s->tests_bvh.p;
     d.prims_bf = s->prims_bf.p;
     d.n_tri = nt;
     d.n_sph = ns;

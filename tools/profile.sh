@@ -1,0 +1,15 @@
+#!/bin/bash
+# rocprofv3 passes over bench.py (run on the GPU box via tools/gpu_steps.sh):
+#   trace: --kernel-trace --stats;  pmc1/pmc2/pmc3: counter passes (no tracing domains with --pmc)
+# usage: tools/profile.sh TAG [bench args...]
+tag=$1; shift
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+out=gpurun_out/prof_$tag
+mkdir -p "$out"
+set -e
+rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- python3 bench.py --no-cpu-baseline "$@" > "$out/trace.log" 2>&1
+rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY --output-format csv -d "$out/pmc1" -o pmc -- python3 bench.py --no-cpu-baseline "$@" > "$out/pmc1.log" 2>&1
+rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/pmc2" -o pmc -- python3 bench.py --no-cpu-baseline "$@" > "$out/pmc2.log" 2>&1
+rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format csv -d "$out/pmc3" -o pmc -- python3 bench.py --no-cpu-baseline "$@" > "$out/pmc3.log" 2>&1
+echo "profile $tag done"
