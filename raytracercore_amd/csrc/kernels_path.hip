@@ -54,10 +54,10 @@ __device__ __forceinline__ V3 xf_dir(const float4* m, V3 p) { return {dot3(m[0],
 
 struct Best {
     float t;    // world distance (Hit.Distance)
-    int slot;   // primitive slot of the traversal mode, -1 = none
+    int sg;     // slot << 1 | geometric inside (before Invert; selects the flipped normal); -1 = none
     float u, v; // triangle barycentrics | sphere: object-space ray parameter in u | plane: t in u
-    int gin;    // geometric inside before Invert (selects the flipped normal)
 };
+__device__ __forceinline__ int pack_sg(int slot, bool gin) { return (slot << 1) | (int)gin; }
 
 // Triangle via the affine inverse record (TestRec): w(t) = 0 gives t, then (u, v).
 // Inside (Moller-Trumbore's 1/det < 0, Triangle.cs:127) <=> d . n > 0 <=> dw > 0.
@@ -74,10 +74,9 @@ __device__ __forceinline__ void hit_tri(const TestRec& R, int slot, V3 o, V3 d, 
     ok &= (fl & F_MIRROR) ? ((u <= 1.0f) & (v <= 1.0f)) : (u + v <= 1.0f);
     if (!(fl & F_TWOSIDED)) ok &= !(gin ^ ((fl & F_INVERT) != 0)); // one-sided: cull Inside
     b.t = ok ? t : b.t;
-    b.slot = ok ? slot : b.slot;
+    b.sg = ok ? pack_sg(slot, gin) : b.sg;
     b.u = ok ? u : b.u;
     b.v = ok ? v : b.v;
-    b.gin = ok ? (int)gin : b.gin;
 }
 
 // Sphere (Sphere.cs:50-155).  Primitive.RayTrace returns the first surviving root: the close
@@ -113,9 +112,8 @@ __device__ __forceinline__ void hit_sph(const TestRec& R, int slot, V3 o, V3 d, 
     const float tw = tc * k;
     const bool ok = (use_close | use_far) & (tw < b.t);
     b.t = ok ? tw : b.t;
-    b.slot = ok ? slot : b.slot;
+    b.sg = ok ? pack_sg(slot, use_far) : b.sg;
     b.u = ok ? tc : b.u;
-    b.gin = ok ? (int)use_far : b.gin;
 }
 
 // Plane (Plane.cs:36-66), including the NearlyEqual branch for rays in the plane.
@@ -134,9 +132,84 @@ __device__ __forceinline__ void hit_plane(const TestRec& R, int slot, V3 o, V3 d
     bool ok = any & (id != prev) & (dist < b.t);
     if (!(fl & F_TWOSIDED)) ok &= !(gin ^ ((fl & F_INVERT) != 0));
     b.t = ok ? dist : b.t;
-    b.slot = ok ? slot : b.slot;
+    b.sg = ok ? pack_sg(slot, gin) : b.sg;
     b.u = ok ? (flat ? 0.0f : t) : b.u;
-    b.gin = ok ? (int)gin : b.gin;
+}
+
+// Axis-aligned rectangle on plane `AXIS` (RectRec): the same hit as the Mirror parallelogram
+// test (u, v in [0, 1]^2) with the extents in world units.  id = 1 / d, oi = o / d.
+template <int AXIS>
+__device__ __forceinline__ void hit_rect(const RectRec& R, int slot, V3 o, V3 d, V3 id, V3 oi, bool dpos, bool dneg,
+                                         int prev, Best& b)
+{
+    const float ida = AXIS == 0 ? id.x : AXIS == 1 ? id.y : id.z;
+    const float oia = AXIS == 0 ? oi.x : AXIS == 1 ? oi.y : oi.z;
+    const float d1 = AXIS == 0 ? d.y : d.x, o1 = AXIS == 0 ? o.y : o.x;
+    const float d2 = AXIS == 2 ? d.y : d.z, o2 = AXIS == 2 ? o.y : o.z;
+    const float t = fmaf(R.c, ida, -oia);
+    const float p1 = fmaf(t, d1, o1), p2 = fmaf(t, d2, o2);
+    const bool gin = R.nsign > 0.0f ? dpos : dneg; // d . N > 0 (per-ray masks, uniform select)
+    bool ok = (t >= 0.0f) & (t < b.t) & (p1 >= R.lo1) & (p1 <= R.hi1) & (p2 >= R.lo2) & (p2 <= R.hi2) &
+              (R.id != prev);
+    if (!(R.flags & F_TWOSIDED)) ok &= !(gin ^ ((R.flags & F_INVERT) != 0));
+    b.t = ok ? t : b.t; // the shading step rebuilds the hit point from t
+    b.sg = ok ? pack_sg(slot, gin) : b.sg;
+}
+
+// Every primitive in slot order; each group's records are prefetched one iteration ahead
+// (scalar loads of record i+1 overlap the tests of record i).
+__device__ __forceinline__ void trace_brute(const PathScene& s, const TestRec* __restrict__ tests,
+                                            const RectRec* __restrict__ rects, const XformF* __restrict__ xf, V3 o,
+                                            V3 d, int prev, Best& b)
+{
+    int i = 0;
+    const int nr = s.n_rect[0] + s.n_rect[1] + s.n_rect[2];
+    if (nr > 0) {
+        const V3 id = v3(rcp(d.x), rcp(d.y), rcp(d.z));
+        const V3 oi = o * id;
+        RectRec cur = rects[0];
+        int end = s.n_rect[0];
+        bool dp = d.x > 0.0f, dn = d.x < 0.0f;
+        for (; i < end; i++) {
+            const RectRec nxt = rects[i + 1];
+            hit_rect<0>(cur, i, o, d, id, oi, dp, dn, prev, b);
+            cur = nxt;
+        }
+        end += s.n_rect[1];
+        dp = d.y > 0.0f;
+        dn = d.y < 0.0f;
+        for (; i < end; i++) {
+            const RectRec nxt = rects[i + 1];
+            hit_rect<1>(cur, i, o, d, id, oi, dp, dn, prev, b);
+            cur = nxt;
+        }
+        end += s.n_rect[2];
+        dp = d.z > 0.0f;
+        dn = d.z < 0.0f;
+        for (; i < end; i++) {
+            const RectRec nxt = rects[i + 1];
+            hit_rect<2>(cur, i, o, d, id, oi, dp, dn, prev, b);
+            cur = nxt;
+        }
+    }
+    int end = i + s.n_tri;
+    if (i < end) {
+        TestRec cur = tests[i];
+        for (; i < end; i++) {
+            const TestRec nxt = tests[i + 1];
+            hit_tri(cur, i, o, d, prev, b);
+            cur = nxt;
+        }
+    }
+    end = i + s.n_sph;
+    if (i < end) {
+        TestRec cur = tests[i];
+        for (; i < end; i++) {
+            const TestRec nxt = tests[i + 1];
+            hit_sph(cur, i, o, d, prev, xf, b);
+            cur = nxt;
+        }
+    }
 }
 
 __device__ __forceinline__ void hit_any(const TestRec& R, int slot, V3 o, V3 d, int prev, const XformF* __restrict__ xf,
@@ -284,12 +357,13 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
                                      const XformF* __restrict__ xfs, const float4* __restrict__ vnormals, const Best& b,
                                      Sample& S, V3& col)
 {
-    if (b.slot < 0) {
+    if (b.sg < 0) {
         if (S.bounce == 0 || s.ambient_miss) return 2;
         col = v3(s.ambient_r, s.ambient_g, s.ambient_b);
         return 1;
     }
-    const PrimF P = prims[b.slot];
+    const bool gin = (b.sg & 1) != 0;
+    const PrimF P = prims[b.sg >> 1];
     const uint32_t fl = __float_as_uint(P.b.w);
     const int id = __float_as_int(P.a.w);
     const MatF& M = mats[id];
@@ -306,13 +380,21 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
     // hit position and normal facing the incoming ray
     V3 pos, nrm;
     if (kind == RT_PRIM_TRIANGLE) {
-        pos = madd(xyz(P.b), b.u, madd(xyz(P.c), b.v, xyz(P.a)));
+        const uint32_t axis = (fl & F_AXIS_MASK) >> F_AXIS_SHIFT;
+        if (axis) { // axis-aligned rectangle hit (hit_rect): on the plane through Vert0
+            pos = madd(S.d, b.t, S.o);
+            if (axis == 1) pos.x = P.a.x;
+            else if (axis == 2) pos.y = P.a.y;
+            else pos.z = P.a.z;
+        } else {
+            pos = madd(xyz(P.b), b.u, madd(xyz(P.c), b.v, xyz(P.a)));
+        }
         if (fl & F_HASNORMALS) { // Triangle.GetNormal quirk: Normal is never set -> NaN when inside
             const float4* vn = vnormals + 3 * id;
             nrm = normalize(madd(xyz(vn[2]), b.u + b.v, madd(xyz(vn[1]), b.v, xyz(vn[0]) * b.u)));
-            if (b.gin) nrm = v3(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
+            if (gin) nrm = v3(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
         } else {
-            nrm = b.gin ? -xyz(P.d) : xyz(P.d);
+            nrm = gin ? -xyz(P.d) : xyz(P.d);
         }
     } else if (kind == RT_PRIM_SPHERE) {
         V3 oo = S.o, dd = S.d;
@@ -330,12 +412,12 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
         } else {
             pos = op;
         }
-        nrm = b.gin ? -n : n;
+        nrm = gin ? -n : n;
     } else {
         pos = madd(S.d, b.u, S.o);
-        nrm = b.gin ? -xyz(P.a) : xyz(P.a);
+        nrm = gin ? -xyz(P.a) : xyz(P.a);
     }
-    const bool inside = b.gin ^ ((fl & F_INVERT) != 0);
+    const bool inside = gin ^ ((fl & F_INVERT) != 0);
 
     // RandomShine (Raytracer.cs:51-56): z = U^(1/shininess), theta = U * 2pi
     const float shin = M.shininess;
@@ -408,17 +490,36 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
 #ifndef RT_PATH_WAVES
 #define RT_PATH_WAVES 4 // minimum waves per SIMD the register allocator must allow
 #endif
-template <int TRAV, int STACK, bool STATS>
+// LDS: stage the shading records (PrimF per slot, MatF per ID, XformF) in LDS so that the
+// per-lane gathers after each closest-hit query are LDS reads instead of dependent global loads.
+template <int TRAV, int STACK, bool LDS, bool STATS>
 __global__ void __launch_bounds__(256, RT_PATH_WAVES)
     path_kernel(PathScene s, CameraF cam, PathParams p, const TestRec* __restrict__ tests,
-                const PrimF* __restrict__ prims, const NodeF* __restrict__ nodes, const XformF* __restrict__ xf,
-                const MatF* __restrict__ mats, const float4* __restrict__ vnormals)
+                const RectRec* __restrict__ rects, const PrimF* __restrict__ prims_g, const NodeF* __restrict__ nodes,
+                const XformF* __restrict__ xf, const MatF* __restrict__ mats_g, const float4* __restrict__ vnormals)
 {
     __shared__ int stack_mem[TRAV == RT_TRAVERSAL_BVH ? STACK * 256 : 1];
+    extern __shared__ float4 lds_scene[];
     int* stk = stack_mem + threadIdx.x;
+    const PrimF* __restrict__ prims = prims_g;
+    const MatF* __restrict__ mats = mats_g;
+    const XformF* __restrict__ xfs = xf;
+    if (LDS) {
+        const int n_p = s.n_slots * 4, n_m = s.n_ids * 5, n_x = s.n_xf * 9;
+        const float4* gp = reinterpret_cast<const float4*>(prims_g);
+        const float4* gm = reinterpret_cast<const float4*>(mats_g);
+        const float4* gx = reinterpret_cast<const float4*>(xf);
+        for (int i = threadIdx.x; i < n_p; i += 256) lds_scene[i] = gp[i];
+        for (int i = threadIdx.x; i < n_m; i += 256) lds_scene[n_p + i] = gm[i];
+        for (int i = threadIdx.x; i < n_x; i += 256) lds_scene[n_p + n_m + i] = gx[i];
+        __syncthreads();
+        prims = reinterpret_cast<const PrimF*>(lds_scene);
+        mats = reinterpret_cast<const MatF*>(lds_scene + n_p);
+        xfs = reinterpret_cast<const XformF*>(lds_scene + n_p + n_m);
+    }
     const int lane = threadIdx.x & 63;
     const unsigned total = (unsigned)p.n_chunks * (unsigned)p.n_pad;
-    const int pln0 = s.n_tri + s.n_sph;
+    const int pln0 = s.n_bvh;
 
     bool active = true, item_open = false, live = false;
     unsigned item = 0;
@@ -473,21 +574,20 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
             live = true;
         }
         if (live) {
-            Best b{__builtin_huge_valf(), -1, 0.0f, 0.0f, 0};
+            Best b{__builtin_huge_valf(), -1, 0.0f, 0.0f};
             if (TRAV == RT_TRAVERSAL_BVH) {
                 trace_bvh<STACK, STATS>(s, nodes, tests, xf, S.o, S.d, S.prev, b, stk, cnt);
             } else {
-                for (int i = 0; i < s.n_tri; i++) hit_tri(tests[i], i, S.o, S.d, S.prev, b);
-                for (int i = s.n_tri; i < pln0; i++) hit_sph(tests[i], i, S.o, S.d, S.prev, xf, b);
+                trace_brute(s, tests, rects, xf, S.o, S.d, S.prev, b);
                 if (STATS) {
-                    cnt.tris += s.n_tri;
+                    cnt.tris += s.n_rect[0] + s.n_rect[1] + s.n_rect[2] + s.n_tri;
                     cnt.sphs += s.n_sph;
                 }
             }
             for (int i = pln0; i < pln0 + s.n_pln; i++) hit_plane(tests[i], i, S.o, S.d, S.prev, b);
             rays++;
             V3 col;
-            const int r = shade(s, prims, mats, xf, vnormals, b, S, col);
+            const int r = shade(s, prims, mats, xfs, vnormals, b, S, col);
             if (r != 0) {
                 if (r == 1) {
                     ar += col.x;
@@ -560,45 +660,39 @@ __global__ void colors_1spp_kernel(PathParams p, double* out)
     out[o + 2] = miss ? -1.0 : (double)v.z;
 }
 
-using PathKernel = void (*)(PathScene, CameraF, PathParams, const TestRec*, const PrimF*, const NodeF*,
-                            const XformF*, const MatF*, const float4*);
+using PathKernel = void (*)(PathScene, CameraF, PathParams, const TestRec*, const RectRec*, const PrimF*,
+                            const NodeF*, const XformF*, const MatF*, const float4*);
 
-// variant: 0 brute force, 1 BVH with a 24-entry stack, 2 BVH with a 48-entry stack
+template <int TRAV, int STACK, bool LDS>
+PathKernel pick_stats(bool stats)
+{
+    return stats ? path_kernel<TRAV, STACK, LDS, true> : path_kernel<TRAV, STACK, LDS, false>;
+}
+
+// variant = traversal * 2 + lds; traversal 0 brute force, 1 BVH (24-entry stack), 2 BVH (48)
 PathKernel pick(int variant, bool stats)
 {
     switch (variant) {
-    case 1: return stats ? path_kernel<RT_TRAVERSAL_BVH, 24, true> : path_kernel<RT_TRAVERSAL_BVH, 24, false>;
-    case 2: return stats ? path_kernel<RT_TRAVERSAL_BVH, 48, true> : path_kernel<RT_TRAVERSAL_BVH, 48, false>;
-    default: return stats ? path_kernel<RT_TRAVERSAL_BRUTE, 1, true> : path_kernel<RT_TRAVERSAL_BRUTE, 1, false>;
+    case 1: return pick_stats<RT_TRAVERSAL_BRUTE, 1, true>(stats);
+    case 2: return pick_stats<RT_TRAVERSAL_BVH, 24, false>(stats);
+    case 3: return pick_stats<RT_TRAVERSAL_BVH, 24, true>(stats);
+    case 4: return pick_stats<RT_TRAVERSAL_BVH, 48, false>(stats);
+    case 5: return pick_stats<RT_TRAVERSAL_BVH, 48, true>(stats);
+    default: return pick_stats<RT_TRAVERSAL_BRUTE, 1, false>(stats);
     }
 }
 
-} // namespace
-
-int path_variant(int traversal, int bvh_depth)
-{
-    if (traversal != RT_TRAVERSAL_BVH) return 0;
-    return bvh_depth < 24 ? 1 : 2;
-}
-
-int path_blocks_per_cu(int variant, bool stats)
-{
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(pick(variant, stats)), 256, 0) !=
-            hipSuccess ||
-        n < 1)
-        n = 1;
-    return n;
-}
-
-hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& p, int variant, int grid_blocks,
-                       hipStream_t stream, bool stats)
+PathScene make_path_scene(const DevScene& s)
 {
     PathScene ps;
+    for (int k = 0; k < 3; k++) ps.n_rect[k] = s.n_rect[k];
     ps.n_tri = s.n_tri;
     ps.n_sph = s.n_sph;
     ps.n_pln = s.n_pln;
-    ps.n_bvh = s.n_tri + s.n_sph;
+    ps.n_bvh = s.n_rect[0] + s.n_rect[1] + s.n_rect[2] + s.n_tri + s.n_sph;
+    ps.n_slots = ps.n_bvh + s.n_pln;
+    ps.n_ids = s.n_ids;
+    ps.n_xf = s.n_xf;
     ps.root = s.root;
     ps.width = s.width;
     ps.recursion = s.recursion;
@@ -608,17 +702,50 @@ hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& 
     ps.ambient_r = s.ambient.x;
     ps.ambient_g = s.ambient.y;
     ps.ambient_b = s.ambient.z;
+    return ps;
+}
+
+} // namespace
+
+size_t path_lds_bytes(const DevScene& s)
+{
+    const size_t slots = (size_t)s.n_rect[0] + s.n_rect[1] + s.n_rect[2] + s.n_tri + s.n_sph + s.n_pln;
+    return slots * sizeof(PrimF) + (size_t)s.n_ids * sizeof(MatF) + (size_t)s.n_xf * sizeof(XformF);
+}
+
+int path_variant(int traversal, int bvh_depth, bool lds)
+{
+    const int t = traversal != RT_TRAVERSAL_BVH ? 0 : (bvh_depth < 24 ? 1 : 2);
+    return t * 2 + (lds ? 1 : 0);
+}
+
+int path_blocks_per_cu(int variant, size_t dyn_lds, bool stats)
+{
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(pick(variant, stats)), 256,
+                                                     (variant & 1) ? dyn_lds : 0) != hipSuccess ||
+        n < 1)
+        n = 1;
+    return n;
+}
+
+hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& p, int variant, int grid_blocks,
+                       hipStream_t stream, bool stats)
+{
+    PathScene ps = make_path_scene(s);
     CameraF ca = cam;
     PathParams pa = p;
-    const bool bvh = variant != 0;
+    const bool bvh = variant >= 2;
     const TestRec* tests = bvh ? s.tests_bvh : s.tests_bf;
+    const RectRec* rects = s.rects_bf;
     const PrimF* prims = bvh ? s.prims_bvh : s.prims_bf;
     const NodeF* nodes = s.nodes;
     const XformF* xf = s.xf;
     const MatF* mats = s.mats;
     const float4* vn = s.vnormals;
-    void* args[] = {&ps, &ca, &pa, &tests, &prims, &nodes, &xf, &mats, &vn};
-    return hipLaunchKernel(reinterpret_cast<const void*>(pick(variant, stats)), dim3(grid_blocks), dim3(256), args, 0,
+    void* args[] = {&ps, &ca, &pa, &tests, &rects, &prims, &nodes, &xf, &mats, &vn};
+    const size_t dyn = (variant & 1) ? path_lds_bytes(s) : 0;
+    return hipLaunchKernel(reinterpret_cast<const void*>(pick(variant, stats)), dim3(grid_blocks), dim3(256), args, dyn,
                            stream);
 }
 

@@ -23,6 +23,20 @@ enum : uint32_t {
     F_INVERT = 1u << 4,
     F_HASNORMALS = 1u << 5,
     F_TRANSFORMED = 1u << 6,
+    F_AXIS_SHIFT = 7,   // axis-aligned rectangle: (axis + 1) in bits 7-8, 0 = general
+    F_AXIS_MASK = 3u << 7,
+};
+
+// Axis-aligned rectangle (a Mirror parallelogram whose edges follow two coordinate axes, e.g.
+// every Cube face, Cube.cs:90-116): the plane coordinate on `axis`, the extents on the two
+// other axes (in x, y, z order) and the side the face normal points to.
+struct alignas(16) RectRec {
+    float c;        // plane coordinate
+    float lo1, hi1; // extent on the first remaining axis
+    float lo2, hi2; // extent on the second remaining axis
+    float nsign;    // +1 if the face normal points along +axis, else -1
+    int32_t id;     // primitive ID
+    uint32_t flags;
 };
 
 // ---- exact fp64 scene (primary-ID pass) -----------------------------------------------
@@ -91,8 +105,13 @@ struct alignas(16) TestRec {
 // Scalar fields of the path kernel (pointers are passed as separate __restrict__ arguments
 // so that the wave-uniform primitive loop is served by scalar loads).
 struct PathScene {
-    int32_t n_tri, n_sph, n_pln; // brute-force order: triangles | spheres | planes
+    // brute-force slot order: x-rects | y-rects | z-rects | triangles | spheres | planes
+    int32_t n_rect[3];
+    int32_t n_tri, n_sph, n_pln;
     int32_t n_bvh;               // primitives in the BVH (all but planes); planes follow them
+    int32_t n_slots;             // n_bvh + n_pln (PrimF records)
+    int32_t n_ids;               // primitive IDs (MatF records)
+    int32_t n_xf;                // XformF records
     int32_t root;                // child reference of the BVH root
     int32_t width;               // frame width (RNG pixel index)
     int32_t recursion;
@@ -128,8 +147,10 @@ struct DevScene {
     // fast set; slot order is [triangles | spheres | planes] for brute force and
     // [BVH leaf order | planes] for the BVH, with matching TestRec / PrimF arrays
     const TestRec* tests_bf;
+    const RectRec* rects_bf;    // slots [0, n_rect[0] + n_rect[1] + n_rect[2])
     const PrimF* prims_bf;
-    int32_t n_tri, n_sph, n_pln;
+    int32_t n_rect[3];
+    int32_t n_tri, n_sph, n_pln; // n_tri counts general triangles only
     const TestRec* tests_bvh;
     const PrimF* prims_bvh;
     const NodeF* nodes;
@@ -138,6 +159,8 @@ struct DevScene {
     const XformF* xf;
     const MatF* mats;
     const float4* vnormals;     // 3 per primitive ID (HasNormals triangles)
+    int32_t n_ids;              // MatF records
+    int32_t n_xf;               // XformF records
     // exact set
     const PrimD* prims_d;
     const XformD* xf_d;

@@ -26,11 +26,12 @@ hipError_t launch_primary_ids(const DevScene& s, const CameraD& cam, int x0, int
                               hipStream_t stream);
 
 // Kernel variant for a traversal mode and BVH depth (the LDS stack must exceed the depth).
-int path_variant(int traversal, int bvh_depth);
+int path_variant(int traversal, int bvh_depth, bool lds);
+size_t path_lds_bytes(const DevScene& s);   // dynamic LDS of the staged (lds) variants
 // Launch the persistent kernel; stats counts node visits / primitive tests (slower build).
 hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& p, int variant, int grid_blocks,
                        hipStream_t stream, bool stats);
-int path_blocks_per_cu(int variant, bool stats);
+int path_blocks_per_cu(int variant, size_t dyn_lds, bool stats);
 
 // partial -> fp64 planar accumulators (d_sum[3][w*h], d_samples, d_misses), added to.
 hipError_t launch_accumulate(const PathParams& p, double* d_sum, uint32_t* d_samples, uint32_t* d_misses,

@@ -75,6 +75,7 @@ float as_f(uint32_t v)
     return f;
 }
 double luminance(rt_color c) { return 0.299 * c.r + 0.587 * c.g + 0.114 * c.b; } // DoubleColor.cs:76-79
+uint32_t p_flags_with_axis(uint32_t flags, int axis) { return flags | ((uint32_t)(axis + 1) << F_AXIS_SHIFT); }
 
 } // namespace
 
@@ -91,6 +92,7 @@ struct rt_scene {
     DevScene dev{};
     DevBuf<PrimF> prims_bf, prims_bvh;
     DevBuf<TestRec> tests_bf, tests_bvh;
+    DevBuf<RectRec> rects_bf;
     DevBuf<NodeF> nodes;
     DevBuf<XformF> xf;
     DevBuf<MatF> mats;
@@ -217,16 +219,62 @@ int upload_scene(rt_scene* s)
         }
         return t;
     };
+    // An axis-aligned rectangle: a Mirror parallelogram with both edges on coordinate axes.
+    auto rect_axis = [&](int i) {
+        const HostPrim& p = H[i];
+        if (p.kind != RT_PRIM_TRIANGLE || !(p.flags & F_MIRROR) || (p.flags & F_HASNORMALS)) return -1;
+        const double e1[3] = {p.e01.x, p.e01.y, p.e01.z}, e2[3] = {p.e02.x, p.e02.y, p.e02.z};
+        for (int k = 0; k < 3; k++) {
+            const int a = (k + 1) % 3, b = (k + 2) % 3;
+            if (e1[k] != 0 || e2[k] != 0) continue;
+            const bool e1a = e1[a] != 0 && e1[b] == 0, e1b = e1[b] != 0 && e1[a] == 0;
+            const bool e2a = e2[a] != 0 && e2[b] == 0, e2b = e2[b] != 0 && e2[a] == 0;
+            if ((e1a && e2b) || (e1b && e2a)) return k;
+        }
+        return -1;
+    };
+    auto rectrec = [&](int i, int k) {
+        const HostPrim& p = H[i];
+        const double v0[3] = {p.v[0].x, p.v[0].y, p.v[0].z}, e1[3] = {p.e01.x, p.e01.y, p.e01.z},
+                     e2[3] = {p.e02.x, p.e02.y, p.e02.z}, nn[3] = {p.n.x, p.n.y, p.n.z};
+        const int a1 = k == 0 ? 1 : 0, a2 = k == 2 ? 1 : 2; // the other two axes in x, y, z order
+        RectRec r;
+        r.c = (float)v0[k];
+        const double c1[4] = {v0[a1], v0[a1] + e1[a1], v0[a1] + e2[a1], v0[a1] + e1[a1] + e2[a1]};
+        const double c2[4] = {v0[a2], v0[a2] + e1[a2], v0[a2] + e2[a2], v0[a2] + e1[a2] + e2[a2]};
+        r.lo1 = (float)std::min(std::min(c1[0], c1[1]), std::min(c1[2], c1[3]));
+        r.hi1 = (float)std::max(std::max(c1[0], c1[1]), std::max(c1[2], c1[3]));
+        r.lo2 = (float)std::min(std::min(c2[0], c2[1]), std::min(c2[2], c2[3]));
+        r.hi2 = (float)std::max(std::max(c2[0], c2[1]), std::max(c2[2], c2[3]));
+        r.nsign = nn[k] > 0 ? 1.0f : -1.0f;
+        r.id = i;
+        r.flags = p.flags;
+        return r;
+    };
     std::vector<PrimF> bf, bv;
     std::vector<TestRec> tbf, tbv;
-    int nt = 0, ns = 0, np = 0;
-    for (int kind = 0; kind < 3; kind++)
-        for (int i = 0; i < n; i++)
-            if (H[i].kind == kind) {
-                bf.push_back(primf(i));
-                tbf.push_back(testrec(i));
-                (kind == 0 ? nt : kind == 1 ? ns : np)++;
+    std::vector<RectRec> rects;
+    int nr[3] = {0, 0, 0}, nt = 0, ns = 0, np = 0;
+    std::vector<int> group(n);
+    for (int i = 0; i < n; i++) {
+        const int ax = rect_axis(i);
+        group[i] = ax >= 0 ? ax : (H[i].kind == RT_PRIM_TRIANGLE ? 3 : H[i].kind == RT_PRIM_SPHERE ? 4 : 5);
+    }
+    for (int g = 0; g < 6; g++)
+        for (int i = 0; i < n; i++) {
+            if (group[i] != g) continue;
+            PrimF f = primf(i);
+            if (g < 3) {
+                const uint32_t fl = p_flags_with_axis(H[i].flags, g);
+                std::memcpy(&f.b.w, &fl, 4);
+                rects.push_back(rectrec(i, g));
+                nr[g]++;
+            } else {
+                (g == 3 ? nt : g == 4 ? ns : np)++;
             }
+            bf.push_back(f);
+            tbf.push_back(testrec(i));
+        }
     for (int i : s->sah.order) {
         bv.push_back(primf(i));
         tbv.push_back(testrec(i));
@@ -257,8 +305,12 @@ int upload_scene(rt_scene* s)
     HIP_TRY(s->ref_nodes.upload(s->ref.nodes));
     HIP_TRY(s->prims_bf.upload(bf));
     HIP_TRY(s->prims_bvh.upload(bv));
+    tbf.push_back(TestRec{}); // spare records: the brute-force loops prefetch one ahead
+    tbv.push_back(TestRec{});
     HIP_TRY(s->tests_bf.upload(tbf));
     HIP_TRY(s->tests_bvh.upload(tbv));
+    rects.push_back(RectRec{}); // one spare record: the kernel prefetches one past each group
+    HIP_TRY(s->rects_bf.upload(rects));
     HIP_TRY(s->nodes.upload(s->sah.nodes));
     HIP_TRY(s->xf.upload(xf));
     HIP_TRY(s->mats.upload(mats));
@@ -270,7 +322,9 @@ int upload_scene(rt_scene* s)
     DevScene& d = s->dev;
     d.tests_bf = s->tests_bf.p;
     d.tests_bvh = s->tests_bvh.p;
+    d.rects_bf = s->rects_bf.p;
     d.prims_bf = s->prims_bf.p;
+    for (int k = 0; k < 3; k++) d.n_rect[k] = nr[k];
     d.n_tri = nt;
     d.n_sph = ns;
     d.n_pln = np;
@@ -281,6 +335,8 @@ int upload_scene(rt_scene* s)
     d.xf = s->xf.p;
     d.mats = s->mats.p;
     d.vnormals = s->vnormals.p;
+    d.n_ids = n;
+    d.n_xf = (int)xf.size();
     d.prims_d = s->prims_d.p;
     d.xf_d = s->xf_d.p;
     d.ref_nodes = s->ref_nodes.p;
@@ -299,14 +355,25 @@ int upload_scene(rt_scene* s)
 int resolve_traversal(rt_scene* s)
 {
     int t = s->traversal;
-    if (t == RT_TRAVERSAL_AUTO) t = (s->dev.n_tri + s->dev.n_sph) <= 48 ? RT_TRAVERSAL_BRUTE : RT_TRAVERSAL_BVH;
+    if (t == RT_TRAVERSAL_AUTO) {
+        const int n_bvh = s->dev.n_rect[0] + s->dev.n_rect[1] + s->dev.n_rect[2] + s->dev.n_tri + s->dev.n_sph;
+        t = n_bvh <= 48 ? RT_TRAVERSAL_BRUTE : RT_TRAVERSAL_BVH;
+    }
     if (t == RT_TRAVERSAL_BVH && s->sah.depth >= 48) {
         set_error("BVH deeper than the kernel's LDS stack");
         return RT_ERR_ARG;
     }
     s->resolved = t;
-    s->variant = path_variant(t, s->sah.depth);
-    s->blocks_per_cu = path_blocks_per_cu(s->variant, false);
+    // Stage the shading records in LDS when that costs no occupancy (RTCORE_PATH_LDS=0/1 forces
+    // the choice for A/B measurements).
+    const size_t lds = path_lds_bytes(s->dev);
+    const int plain = path_variant(t, s->sah.depth, false), staged = path_variant(t, s->sah.depth, true);
+    const int occ_plain = path_blocks_per_cu(plain, 0, false);
+    const int occ_staged = lds <= 64 * 1024 ? path_blocks_per_cu(staged, lds, false) : 0;
+    bool use_lds = occ_staged >= occ_plain;
+    if (const char* e = getenv("RTCORE_PATH_LDS")) use_lds = e[0] == '1' && occ_staged > 0;
+    s->variant = use_lds ? staged : plain;
+    s->blocks_per_cu = use_lds ? occ_staged : occ_plain;
     return RT_OK;
 }
 
