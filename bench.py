@@ -63,7 +63,7 @@ def cpu_baseline(cfg_name: str, threads: int):
     orc = OracleScene.from_file(rc.scene_path(scene_file))
     orc.set_size(W, H)
     orc.select_camera(cam)
-    spp = 4 if W * H > 100000 else 16
+    spp = 16 if W * H > 100000 else 64  # a few seconds on 16 host threads
     _, n, m, rays, secs, used = orc.render_frame(spp, seed=0, threads=threads)
     return {
         "value": round(rays / secs / 1e6, 3),
