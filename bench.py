@@ -32,26 +32,44 @@ CONFIGS = {
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 vector = fp32 MFMA dense peak
 
 
-def flops_per_ray(info, scene) -> float:
-    """SURVEY.md §8(d) compute view: 20*N_node + 45*N_tri + 30*N_sph (+60 per transformed sphere) + 150."""
+def scene_counts(scene):
     import raytracercore_amd as rc
 
-    n_tri = sum(1 for p in scene.prims if p.kind == rc.RT_PRIM_TRIANGLE)
-    n_sph = sum(1 for p in scene.prims if p.kind == rc.RT_PRIM_SPHERE)
+    kinds = [p.kind for p in scene.prims]
     n_xf = sum(1 for p in scene.prims if p.kind == rc.RT_PRIM_SPHERE and p.flags & rc.RT_FLAG_TRANSFORMED)
-    n_pln = sum(1 for p in scene.prims if p.kind == rc.RT_PRIM_PLANE)
-    # brute force tests every primitive on every ray
-    return 45.0 * n_tri + 30.0 * (n_sph + n_pln) + 60.0 * n_xf + 150.0
+    return kinds.count(rc.RT_PRIM_TRIANGLE), kinds.count(rc.RT_PRIM_SPHERE), kinds.count(rc.RT_PRIM_PLANE), n_xf
 
 
-def bytes_per_ray(scene) -> float:
-    """SURVEY.md §8(d) B_ray for brute force (N_node = 0, every primitive tested)."""
-    import raytracercore_amd as rc
+def flops_per_ray(st, scene) -> float:
+    """SURVEY.md §8(d) compute view: 20*N_node + 45*N_tri + 30*N_sph (+60 per transformed sphere) + 150,
+    with N_* the node visits / primitive tests per ray segment measured by the instrumented kernel."""
+    n_tri, n_sph, n_pln, n_xf = scene_counts(scene)
+    xf_share = n_xf / n_sph if n_sph else 0.0
+    return (20.0 * st["nodes"] + 45.0 * st["tris"] + 30.0 * st["sphs"] * (1.0 + 2.0 * xf_share)
+            + 30.0 * n_pln + 150.0)
 
-    n_tri = sum(1 for p in scene.prims if p.kind == rc.RT_PRIM_TRIANGLE)
-    n_sph = sum(1 for p in scene.prims if p.kind != rc.RT_PRIM_TRIANGLE)
-    n_xf = sum(1 for p in scene.prims if p.kind == rc.RT_PRIM_SPHERE and p.flags & rc.RT_FLAG_TRANSFORMED)
-    return 32 + 16 + 48.0 * n_tri + 16.0 * n_sph + 144.0 * n_xf + 48
+
+def bytes_per_ray(st, scene) -> float:
+    """SURVEY.md §8(d) B_ray: 32 + 16 + 32*N_node + 48*N_tri + 16*N_sph (+144 transformed) + 48."""
+    n_tri, n_sph, n_pln, n_xf = scene_counts(scene)
+    xf_share = n_xf / n_sph if n_sph else 0.0
+    return 32 + 16 + 32.0 * st["nodes"] + 48.0 * st["tris"] + st["sphs"] * (16.0 + 144.0 * xf_share) + 16.0 * n_pln + 48
+
+
+def path_stats(gpu, W, H, spp, seed, d_bufs):
+    """One untimed instrumented launch: traversal work per ray segment and the wave-cycle split."""
+    d_sum, d_n, d_m, d_rays = d_bufs
+    gpu.set_stats(True)
+    d_rays.zero_()
+    gpu.render_device(0, 0, W, H, spp, seed, 1 << 40, d_sum.data_ptr(), d_n.data_ptr(), d_m.data_ptr(),
+                      d_rays.data_ptr(), 0)
+    st = gpu.get_stats()
+    gpu.set_stats(False)
+    rays = max(1, int(d_rays.item()))
+    cyc = st["cyc_start"] + st["cyc_trace"] + st["cyc_shade"]
+    return {"nodes": st["node_visits"] / rays, "tris": st["tri_tests"] / rays, "sphs": st["sph_tests"] / rays,
+            "cycles": {k: round(st["cyc_" + k] / max(1, cyc), 4) for k in ("start", "trace", "shade")},
+            "wave_iters_per_ray": round(st["wave_iters"] * 64 / rays, 4)}
 
 
 def cpu_baseline(cfg_name: str, threads: int):
@@ -173,9 +191,10 @@ def main() -> int:
             raise SystemExit(f"sample bookkeeping mismatch: {np.unique(n_all + m_all)} != {expect}")
         my_rays_per_step = total_rays / (args.steps * world)
         avg_ms = sum(kernel_ms) / len(kernel_ms)
-        fpr = flops_per_ray(info, scene)
+        st = path_stats(gpu, W, H, max(1, spp // 16), args.seed, (d_sum, d_n, d_m, d_rays))
+        fpr = flops_per_ray(st, scene)
         achieved_tf = fpr * my_rays_per_step / (avg_ms * 1e-3) / 1e12
-        bpr = bytes_per_ray(scene)
+        bpr = bytes_per_ray(st, scene)
         out = {
             "metric": "Mrays/sec (primary+secondary) and samples/sec at 1080p, Cornell box",
             "value": round(total_rays / elapsed / 1e6, 2),
@@ -199,8 +218,10 @@ def main() -> int:
                          "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4), "traffic": None,
                          "note": f"fp32 VALU kernel (no MFMA; the gfx950 fp32 vector and MFMA peaks are both "
                                  f"157.3 TFLOP/s); {fpr:.0f} algorithmic FLOP per ray (SURVEY 8(d)); HBM view "
-                                 f"(SURVEY B_ray {bpr:.0f} B/ray, scene served from the scalar cache): "
+                                 f"(SURVEY B_ray {bpr:.0f} B/ray, scene served on chip): "
                                  f"{bpr * my_rays_per_step / (avg_ms * 1e-3) / 1e9:.0f} GB/s"},
+            "path_stats": {"per_ray": {k: round(st[k], 3) for k in ("nodes", "tris", "sphs")},
+                           "wave_cycle_split": st["cycles"], "wave_iters_per_ray": st["wave_iters_per_ray"]},
         }
         if not args.no_cpu_baseline and world == 1:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)

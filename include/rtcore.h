@@ -202,6 +202,18 @@ int rt_primary_ids_device(rt_scene* scene, int32_t x0, int32_t y0, int32_t w, in
 /* Duration in ms of the last path-tracing kernel launched on this scene (hipEvent pair). */
 int rt_last_kernel_ms(rt_scene* scene, float* ms);
 
+/*
+ * Instrumentation (profiling builds of the measurement, not the render): while enabled, the
+ * path kernel's instrumented variant runs and adds up, over all launches since the last read,
+ *   [0] BVH node visits  [1] triangle tests  [2] sphere tests           (per ray segment)
+ *   [3] wave cycles in work fetch + camera ray  [4] in traversal  [5] in shading
+ *   [6] wave loop iterations
+ * rt_scene_get_stats synchronises the device, copies min(n, RT_STATS_COUNT) counters and zeroes them.
+ */
+#define RT_STATS_COUNT 7
+int rt_scene_set_stats(rt_scene* scene, int32_t enable);
+int rt_scene_get_stats(rt_scene* scene, uint64_t* out, int32_t n);
+
 /* ------------------------------------------------------------- multi-GPU ---- */
 /*
  * Whole frame on n_gpus devices of this process: rows are dealt to devices in

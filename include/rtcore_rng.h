@@ -59,19 +59,28 @@ typedef struct rt_rng {
     uint32_t n;      /* next draw index */
 } rt_rng;
 
-RT_HD uint64_t rt_rng_key(uint64_t seed, uint64_t pixel, uint64_t sample)
-{
-    return rt_splitmix64(rt_splitmix64(rt_splitmix64(seed) + pixel) + sample);
-}
+/* The key factors as seed_key = splitmix64(seed), pixel_key = splitmix64(seed_key + pixel),
+ * key = splitmix64(pixel_key + sample): a kernel hoists the first two out of its sample loop. */
+RT_HD uint64_t rt_rng_pixel_key(uint64_t seed_key, uint64_t pixel) { return rt_splitmix64(seed_key + pixel); }
 
-RT_HD rt_rng rt_rng_init(uint64_t seed, uint64_t pixel, uint64_t sample)
+RT_HD rt_rng rt_rng_from_pixel_key(uint64_t pixel_key, uint64_t sample)
 {
-    uint64_t k = rt_rng_key(seed, pixel, sample);
+    uint64_t k = rt_splitmix64(pixel_key + sample);
     rt_rng r;
     r.k0 = (uint32_t)k;
     r.k1 = (uint32_t)(k >> 32);
     r.n = 0;
     return r;
+}
+
+RT_HD uint64_t rt_rng_key(uint64_t seed, uint64_t pixel, uint64_t sample)
+{
+    return rt_splitmix64(rt_rng_pixel_key(rt_splitmix64(seed), pixel) + sample);
+}
+
+RT_HD rt_rng rt_rng_init(uint64_t seed, uint64_t pixel, uint64_t sample)
+{
+    return rt_rng_from_pixel_key(rt_rng_pixel_key(rt_splitmix64(seed), pixel), sample);
 }
 
 /* 24-bit draw as an integer in [0, 2^24). */

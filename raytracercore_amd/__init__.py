@@ -115,6 +115,8 @@ def load_library(path: str = "") -> C.CDLL:
                              [C.c_void_p] * 4 + [C.c_void_p]),
         "rt_primary_ids_device": (C.c_int, [C.c_void_p] + [C.c_int32] * 4 + [C.c_void_p, C.c_void_p]),
         "rt_last_kernel_ms": (C.c_int, [C.c_void_p, P(C.c_float)]),
+        "rt_scene_set_stats": (C.c_int, [C.c_void_p, C.c_int32]),
+        "rt_scene_get_stats": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_int32]),
         "rt_render_frame_multi": (C.c_int, [P(rt_scene_params), P(rt_prim), C.c_int32, P(rt_camera), C.c_int32,
                                             C.c_int32, C.c_uint64, P(rt_color), P(C.c_uint32), P(C.c_uint32),
                                             P(C.c_uint64)]),
@@ -278,6 +280,18 @@ class GpuRaytracer:
         ms = C.c_float(0)
         _check(self.lib.rt_last_kernel_ms(self.handle, C.byref(ms)))
         return float(ms.value)
+
+    STAT_NAMES = ("node_visits", "tri_tests", "sph_tests", "cyc_start", "cyc_trace", "cyc_shade", "wave_iters")
+
+    def set_stats(self, enable: bool) -> None:
+        """rt_scene_set_stats: run the instrumented kernel variant (profiling only)."""
+        _check(self.lib.rt_scene_set_stats(self.handle, 1 if enable else 0))
+
+    def get_stats(self) -> dict:
+        """rt_scene_get_stats: counters accumulated since the last read (then zeroed)."""
+        out = (C.c_uint64 * len(self.STAT_NAMES))()
+        _check(self.lib.rt_scene_get_stats(self.handle, out, len(self.STAT_NAMES)))
+        return dict(zip(self.STAT_NAMES, (int(v) for v in out)))
 
 
 def render_frame_multi(scene: ParsedScene, camera_index: int, n_gpus: int, spp: int, seed: int = 0,

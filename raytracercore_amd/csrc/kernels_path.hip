@@ -137,60 +137,48 @@ __device__ __forceinline__ void hit_plane(const TestRec& R, int slot, V3 o, V3 d
 }
 
 // Axis-aligned rectangle on plane `AXIS` (RectRec): the same hit as the Mirror parallelogram
-// test (u, v in [0, 1]^2) with the extents in world units.  id = 1 / d, oi = o / d.
+// test (u, v in [0, 1]^2) with the extents in world units.  id = 1 / d, oi = o / d.  The side
+// of the hit (Inside) is not tracked here: the shading step recomputes it from the normal.
 template <int AXIS>
-__device__ __forceinline__ void hit_rect(const RectRec& R, int slot, V3 o, V3 d, V3 id, V3 oi, bool dpos, bool dneg,
-                                         int prev, Best& b)
+__device__ __forceinline__ void hit_rect(const RectRec& R, int sg, V3 o, V3 d, V3 id, V3 oi, int prev, Best& b)
 {
     const float ida = AXIS == 0 ? id.x : AXIS == 1 ? id.y : id.z;
     const float oia = AXIS == 0 ? oi.x : AXIS == 1 ? oi.y : oi.z;
+    const float da = AXIS == 0 ? d.x : AXIS == 1 ? d.y : d.z;
     const float d1 = AXIS == 0 ? d.y : d.x, o1 = AXIS == 0 ? o.y : o.x;
     const float d2 = AXIS == 2 ? d.y : d.z, o2 = AXIS == 2 ? o.y : o.z;
     const float t = fmaf(R.c, ida, -oia);
-    const float p1 = fmaf(t, d1, o1), p2 = fmaf(t, d2, o2);
-    const bool gin = R.nsign > 0.0f ? dpos : dneg; // d . N > 0 (per-ray masks, uniform select)
-    bool ok = (t >= 0.0f) & (t < b.t) & (p1 >= R.lo1) & (p1 <= R.hi1) & (p2 >= R.lo2) & (p2 <= R.hi2) &
-              (R.id != prev);
-    if (!(R.flags & F_TWOSIDED)) ok &= !(gin ^ ((R.flags & F_INVERT) != 0));
+    // |p - mid| <= half on both in-plane axes (false for NaN)
+    const bool in1 = fabsf(fmaf(t, d1, o1) - R.m1) <= R.h1;
+    const bool in2 = fabsf(fmaf(t, d2, o2) - R.m2) <= R.h2;
+    // 0 <= t < best as one unsigned compare of the bit patterns (b.t >= 0; NaN and -t fail)
+    const bool near = __float_as_uint(t) < __float_as_uint(b.t);
+    const bool ok = near & in1 & in2 & (R.cull * da <= 0.0f) & (R.id != prev);
     b.t = ok ? t : b.t; // the shading step rebuilds the hit point from t
-    b.sg = ok ? pack_sg(slot, gin) : b.sg;
+    b.sg = ok ? sg : b.sg;
 }
 
-// Every primitive in slot order; each group's records are prefetched one iteration ahead
-// (scalar loads of record i+1 overlap the tests of record i).
+template <int AXIS>
+__device__ __forceinline__ void rect_group(const RectRec* __restrict__ r, int n, V3 o, V3 d, V3 id, V3 oi, int prev,
+                                           Best& b)
+{
+    for (; n > 0; n--, r++) hit_rect<AXIS>(*r, r->sg, o, d, id, oi, prev, b);
+}
+
+// Every primitive in slot order (x-rects | y-rects | z-rects | triangles | spheres); the
+// loop index is wave-uniform, so the records arrive through scalar loads.
 __device__ __forceinline__ void trace_brute(const PathScene& s, const TestRec* __restrict__ tests,
                                             const RectRec* __restrict__ rects, const XformF* __restrict__ xf, V3 o,
                                             V3 d, int prev, Best& b)
 {
     int i = 0;
-    const int nr = s.n_rect[0] + s.n_rect[1] + s.n_rect[2];
-    if (nr > 0) {
+    if (s.n_rect[0] + s.n_rect[1] + s.n_rect[2] > 0) {
         const V3 id = v3(rcp(d.x), rcp(d.y), rcp(d.z));
         const V3 oi = o * id;
-        RectRec cur = rects[0];
-        int end = s.n_rect[0];
-        bool dp = d.x > 0.0f, dn = d.x < 0.0f;
-        for (; i < end; i++) {
-            const RectRec nxt = rects[i + 1];
-            hit_rect<0>(cur, i, o, d, id, oi, dp, dn, prev, b);
-            cur = nxt;
-        }
-        end += s.n_rect[1];
-        dp = d.y > 0.0f;
-        dn = d.y < 0.0f;
-        for (; i < end; i++) {
-            const RectRec nxt = rects[i + 1];
-            hit_rect<1>(cur, i, o, d, id, oi, dp, dn, prev, b);
-            cur = nxt;
-        }
-        end += s.n_rect[2];
-        dp = d.z > 0.0f;
-        dn = d.z < 0.0f;
-        for (; i < end; i++) {
-            const RectRec nxt = rects[i + 1];
-            hit_rect<2>(cur, i, o, d, id, oi, dp, dn, prev, b);
-            cur = nxt;
-        }
+        rect_group<0>(rects, s.n_rect[0], o, d, id, oi, prev, b);
+        rect_group<1>(rects + s.n_rect[0], s.n_rect[1], o, d, id, oi, prev, b);
+        rect_group<2>(rects + s.n_rect[0] + s.n_rect[1], s.n_rect[2], o, d, id, oi, prev, b);
+        i = s.n_rect[0] + s.n_rect[1] + s.n_rect[2];
     }
     int end = i + s.n_tri;
     if (i < end) {
@@ -235,8 +223,24 @@ __device__ __forceinline__ bool slab(float4 lo, float4 hi, V3 oi, V3 id, float t
 }
 
 struct Counters {
-    unsigned nodes, tris, sphs;
+    unsigned nodes, tris, sphs;                                  // per lane
+    unsigned long long cyc_start, cyc_trace, cyc_shade, iters; // per wave (uniform)
 };
+
+// q = x / d, r = x % d through the fp32 reciprocal plus one correction step (exact for the
+// quotients used here, all far below 2^22).
+__device__ __forceinline__ void divmod(unsigned x, unsigned d, float inv_d, unsigned& q, unsigned& r)
+{
+    q = (unsigned)((float)x * inv_d);
+    r = x - q * d;
+    if ((int)r < 0) {
+        q--;
+        r += d;
+    } else if (r >= d) {
+        q++;
+        r -= d;
+    }
+}
 
 template <int STACK, bool STATS>
 __device__ __forceinline__ void trace_bvh(const PathScene& s, const NodeF* __restrict__ nodes,
@@ -362,7 +366,7 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
         col = v3(s.ambient_r, s.ambient_g, s.ambient_b);
         return 1;
     }
-    const bool gin = (b.sg & 1) != 0;
+    bool gin = (b.sg & 1) != 0;
     const PrimF P = prims[b.sg >> 1];
     const uint32_t fl = __float_as_uint(P.b.w);
     const int id = __float_as_int(P.a.w);
@@ -382,6 +386,7 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
     if (kind == RT_PRIM_TRIANGLE) {
         const uint32_t axis = (fl & F_AXIS_MASK) >> F_AXIS_SHIFT;
         if (axis) { // axis-aligned rectangle hit (hit_rect): on the plane through Vert0
+            gin = dot(S.d, xyz(P.d)) > 0.0f; // Moller-Trumbore's inside = d . N > 0
             pos = madd(S.d, b.t, S.o);
             if (axis == 1) pos.x = P.a.x;
             else if (axis == 2) pos.y = P.a.y;
@@ -523,15 +528,20 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
 
     bool active = true, item_open = false, live = false;
     unsigned item = 0;
-    int px = 0, py = 0, s_next = 0, s_end = 0;
+    int fx = 0, fy = 0, s_next = 0, s_end = 0;
+    unsigned long long pkey = 0; // rt_rng_pixel_key of the open item's pixel
     float ar = 0.0f, ag = 0.0f, ab = 0.0f;
     unsigned n_s = 0, n_m = 0, rays = 0;
-    Counters cnt{0, 0, 0};
+    // the wave's pool of work items: [pool_next, pool_end), refilled 64 at a time
+    unsigned pool_next = 0, pool_end = 0;
+    Counters cnt{};
     Sample S;
     S.prev = -1;
     S.bounce = 0;
 
     while (true) {
+        unsigned long long t0 = 0, t1 = 0, t2 = 0;
+        if (STATS) t0 = __builtin_readcyclecounter();
         const bool need = active && !live && (!item_open || s_next >= s_end);
         if (need && item_open) {
             p.partial[item] = make_float4(ar, ag, ab, __uint_as_float(n_s | (n_m << 16)));
@@ -539,40 +549,50 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
         }
         const unsigned long long m = __ballot(need);
         if (m) {
-            const int leader = __ffsll((long long)m) - 1;
-            unsigned base = 0;
-            if (lane == leader) base = atomicAdd(p.counter, (unsigned)__popcll(m));
-            base = __shfl(base, leader);
+            const unsigned k = (unsigned)__popcll(m), avail = pool_end - pool_next;
+            unsigned fresh = 0;
+            if (k > avail) { // wave-uniform: one atomic refills the pool
+                if (lane == 0) fresh = atomicAdd(p.counter, 64u);
+                fresh = __builtin_amdgcn_readfirstlane(fresh);
+            }
             if (need) {
-                item = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+                const unsigned r = (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+                item = r < avail ? pool_next + r : fresh + (r - avail);
                 if (item >= total) {
                     active = false;
                 } else {
-                    const int c = (int)(item / (unsigned)p.n_pad);
-                    const int q = (int)(item - (unsigned)c * (unsigned)p.n_pad);
-                    const int blk = q >> 6, wi = q & 63;
-                    px = (blk % p.blocks_x) * 8 + (wi & 7);
-                    py = (blk / p.blocks_x) * 8 + (wi >> 3);
+                    unsigned c, q, by, bx;
+                    divmod(item, (unsigned)p.n_pad, p.inv_n_pad, c, q);
+                    divmod(q >> 6, (unsigned)p.blocks_x, p.inv_blocks_x, by, bx);
+                    const int px = (int)bx * 8 + (q & 7), py = (int)by * 8 + ((q >> 3) & 7);
                     if (px < p.w && py < p.h) {
                         item_open = true;
-                        s_next = c * p.chunk;
+                        s_next = (int)c * p.chunk;
                         s_end = min(p.spp, s_next + p.chunk);
                         ar = ag = ab = 0.0f;
                         n_s = n_m = 0;
+                        fx = p.x0 + px;
+                        fy = p.band > 0 ? p.y0 + ((py / p.band) * p.band_stride + p.band_offset) * p.band + py % p.band
+                                        : p.y0 + py;
+                        pkey = rt_rng_pixel_key(p.seed_key, (unsigned long long)fy * (unsigned long long)s.width +
+                                                                (unsigned long long)fx);
                     }
                 }
+            }
+            if (k > avail) {
+                pool_next = fresh + (k - avail);
+                pool_end = fresh + 64u;
+            } else {
+                pool_next += k;
             }
         }
         if (!__any(active)) break;
         if (active && item_open && !live && s_next < s_end) {
-            const int fx = p.x0 + px;
-            const int fy = p.band > 0 ? p.y0 + ((py / p.band) * p.band_stride + p.band_offset) * p.band + py % p.band
-                                      : p.y0 + py;
-            S.rng = rt_rng_init(p.seed, (unsigned long long)fy * (unsigned long long)s.width + (unsigned long long)fx,
-                                p.sample_base + (unsigned long long)s_next);
+            S.rng = rt_rng_from_pixel_key(pkey, p.sample_base + (unsigned long long)s_next);
             start_sample(cam, fx, fy, S);
             live = true;
         }
+        if (STATS) t1 = __builtin_readcyclecounter();
         if (live) {
             Best b{__builtin_huge_valf(), -1, 0.0f, 0.0f};
             if (TRAV == RT_TRAVERSAL_BVH) {
@@ -586,6 +606,7 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
             }
             for (int i = pln0; i < pln0 + s.n_pln; i++) hit_plane(tests[i], i, S.o, S.d, S.prev, b);
             rays++;
+            if (STATS) t2 = __builtin_readcyclecounter();
             V3 col;
             const int r = shade(s, prims, mats, xfs, vnormals, b, S, col);
             if (r != 0) {
@@ -600,6 +621,15 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
                 s_next++;
                 live = false;
             }
+        } else if (STATS) {
+            t2 = __builtin_readcyclecounter();
+        }
+        if (STATS) {
+            const unsigned long long t3 = __builtin_readcyclecounter();
+            cnt.cyc_start += t1 - t0;
+            cnt.cyc_trace += t2 - t1;
+            cnt.cyc_shade += t3 - t2;
+            cnt.iters++;
         }
     }
     // one 64-bit add per wave for the ray count (and the optional traversal counters)
@@ -617,6 +647,10 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
             atomicAdd(p.stats + 0, a);
             atomicAdd(p.stats + 1, t);
             atomicAdd(p.stats + 2, q);
+            atomicAdd(p.stats + 3, cnt.cyc_start);
+            atomicAdd(p.stats + 4, cnt.cyc_trace);
+            atomicAdd(p.stats + 5, cnt.cyc_shade);
+            atomicAdd(p.stats + 6, cnt.iters);
         }
     }
 }

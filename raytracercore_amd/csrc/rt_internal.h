@@ -29,14 +29,15 @@ enum : uint32_t {
 
 // Axis-aligned rectangle (a Mirror parallelogram whose edges follow two coordinate axes, e.g.
 // every Cube face, Cube.cs:90-116): the plane coordinate on `axis`, the extents on the two
-// other axes (in x, y, z order) and the side the face normal points to.
+// other axes (in x, y, z order) and the one-sided culling rule folded into one factor:
+// a hit is kept iff cull * d[axis] <= 0 (0 = two-sided; Primitive.cs:56-61).
 struct alignas(16) RectRec {
     float c;        // plane coordinate
-    float lo1, hi1; // extent on the first remaining axis
-    float lo2, hi2; // extent on the second remaining axis
-    float nsign;    // +1 if the face normal points along +axis, else -1
+    float m1, h1;   // mid-point and half-width on the first remaining axis
+    float m2, h2;   // mid-point and half-width on the second remaining axis
+    float cull;     // 0 two-sided, else +-1: sign(N[axis]), negated for Invert
     int32_t id;     // primitive ID
-    uint32_t flags;
+    int32_t sg;     // slot << 1 (the Best.sg of a hit)
 };
 
 // ---- exact fp64 scene (primary-ID pass) -----------------------------------------------

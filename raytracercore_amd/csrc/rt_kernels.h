@@ -14,12 +14,15 @@ struct PathParams {
     int n_chunks;               // ceil(spp / chunk)
     int blocks_x;               // 8x8 pixel blocks per tile row
     int n_pad;                  // padded pixels per chunk (blocks * 64)
+    float inv_n_pad, inv_blocks_x; // fp32 reciprocals for the item decode
     unsigned long long seed;
+    unsigned long long seed_key;   // rt_splitmix64(seed) (rtcore_rng.h)
     unsigned long long sample_base;
-    unsigned int* counter;      // work-item dispenser (zeroed before launch)
+    unsigned int* counter;      // work-item dispenser (zeroed before launch), handed out 64 at a time
     float4* partial;            // [n_chunks][n_pad]: rgb sums, (samples | misses << 16)
     unsigned long long* rays;   // Scene.RayTrace-equivalents (added to)
-    unsigned long long* stats;  // optional [3]: node visits, triangle tests, sphere tests
+    unsigned long long* stats;  // optional [7]: node visits, triangle tests, sphere tests (per lane);
+                                //   wave cycles in sample start, traversal, shading; wave iterations
 };
 
 hipError_t launch_primary_ids(const DevScene& s, const CameraD& cam, int x0, int y0, int w, int h, int32_t* d_ids,

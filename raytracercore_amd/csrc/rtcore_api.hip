@@ -13,6 +13,7 @@
 #include <thread>
 #include <vector>
 
+#include "../../include/rtcore_rng.h"
 #include "host_scene.h"
 #include "rt_kernels.h"
 
@@ -107,6 +108,9 @@ struct rt_scene {
     DevBuf<double> sum, colors;
     DevBuf<uint32_t> samples, misses;
     DevBuf<int32_t> ids;
+    bool stats_on = false;      // launch the instrumented kernel (rt_scene_set_stats)
+    int stats_blocks_per_cu = 1;
+    DevBuf<unsigned long long> stats_buf;
     CameraD camd{};
     CameraF camf{};
     bool has_camera = false;
@@ -242,13 +246,21 @@ int upload_scene(rt_scene* s)
         r.c = (float)v0[k];
         const double c1[4] = {v0[a1], v0[a1] + e1[a1], v0[a1] + e2[a1], v0[a1] + e1[a1] + e2[a1]};
         const double c2[4] = {v0[a2], v0[a2] + e1[a2], v0[a2] + e2[a2], v0[a2] + e1[a2] + e2[a2]};
-        r.lo1 = (float)std::min(std::min(c1[0], c1[1]), std::min(c1[2], c1[3]));
-        r.hi1 = (float)std::max(std::max(c1[0], c1[1]), std::max(c1[2], c1[3]));
-        r.lo2 = (float)std::min(std::min(c2[0], c2[1]), std::min(c2[2], c2[3]));
-        r.hi2 = (float)std::max(std::max(c2[0], c2[1]), std::max(c2[2], c2[3]));
-        r.nsign = nn[k] > 0 ? 1.0f : -1.0f;
+        // fp32 extents rounded outward, stored as mid-point +- half-width
+        const double lo1 = std::min(std::min(c1[0], c1[1]), std::min(c1[2], c1[3]));
+        const double hi1 = std::max(std::max(c1[0], c1[1]), std::max(c1[2], c1[3]));
+        const double lo2 = std::min(std::min(c2[0], c2[1]), std::min(c2[2], c2[3]));
+        const double hi2 = std::max(std::max(c2[0], c2[1]), std::max(c2[2], c2[3]));
+        r.m1 = (float)(0.5 * (lo1 + hi1));
+        r.h1 = (float)(0.5 * (hi1 - lo1));
+        r.m2 = (float)(0.5 * (lo2 + hi2));
+        r.h2 = (float)(0.5 * (hi2 - lo2));
+        // gin = N[k] * d[k] > 0; one-sided keeps gin == Invert (Primitive.cs:56-61): with
+        // q = +-sign(N[k]) that is q * d[k] <= 0 (d[k] = 0 never hits: t is inf or NaN)
+        const float ns = nn[k] > 0 ? 1.0f : -1.0f;
+        r.cull = (p.flags & F_TWOSIDED) ? 0.0f : ((p.flags & F_INVERT) ? -ns : ns);
         r.id = i;
-        r.flags = p.flags;
+        r.sg = 0; // set once the slot is known
         return r;
     };
     std::vector<PrimF> bf, bv;
@@ -268,6 +280,7 @@ int upload_scene(rt_scene* s)
                 const uint32_t fl = p_flags_with_axis(H[i].flags, g);
                 std::memcpy(&f.b.w, &fl, 4);
                 rects.push_back(rectrec(i, g));
+                rects.back().sg = (int)bf.size() << 1;
                 nr[g]++;
             } else {
                 (g == 3 ? nt : g == 4 ? ns : np)++;
@@ -374,6 +387,7 @@ int resolve_traversal(rt_scene* s)
     if (const char* e = getenv("RTCORE_PATH_LDS")) use_lds = e[0] == '1' && occ_staged > 0;
     s->variant = use_lds ? staged : plain;
     s->blocks_per_cu = use_lds ? occ_staged : occ_plain;
+    if (s->stats_on) s->stats_blocks_per_cu = path_blocks_per_cu(s->variant, lds, true);
     return RT_OK;
 }
 
@@ -386,13 +400,18 @@ PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint6
     p.h = h;
     p.band = 0;
     p.spp = spp;
-    // about 8 chunks per pixel keeps the tail of a launch short while each lane still
-    // amortises its item fetch over several samples
-    p.chunk = std::max(1, std::min(64, (spp + 7) / 8));
+    // a few chunks per pixel keep the tail of a launch short while each lane still amortises
+    // its item fetch over many samples (RTCORE_PATH_CHUNKS overrides the count, for tuning)
+    int chunks = 8;
+    if (const char* e = getenv("RTCORE_PATH_CHUNKS")) chunks = std::max(1, atoi(e));
+    p.chunk = std::max(1, std::min(64, (spp + chunks - 1) / chunks));
     p.n_chunks = (spp + p.chunk - 1) / p.chunk;
     p.blocks_x = (w + 7) / 8;
     p.n_pad = p.blocks_x * ((h + 7) / 8) * 64;
+    p.inv_n_pad = 1.0f / (float)p.n_pad;
+    p.inv_blocks_x = 1.0f / (float)p.blocks_x;
     p.seed = seed;
+    p.seed_key = rt_splitmix64(seed);
     p.sample_base = base;
     return p;
 }
@@ -418,16 +437,20 @@ int check_tile(rt_scene* s, int x0, int y0, int w, int h)
 int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t stream)
 {
     const size_t need = (size_t)p.n_chunks * (size_t)p.n_pad;
+    if (need > 0xFFF00000ull) { // 32-bit work-item counter (plus the pools' overshoot)
+        set_error("tile x spp too large for one launch; split the tile");
+        return RT_ERR_ARG;
+    }
     HIP_TRY(s->partial.reserve(need));
     HIP_TRY(s->counter.reserve(1));
     p.partial = s->partial.p;
     p.counter = s->counter.p;
     p.rays = d_rays;
-    p.stats = nullptr;
+    p.stats = s->stats_on ? s->stats_buf.p : nullptr;
     HIP_TRY(hipMemsetAsync(p.counter, 0, sizeof(unsigned int), stream));
-    int grid = s->n_cu * s->blocks_per_cu;
+    const int grid = s->n_cu * (s->stats_on ? s->stats_blocks_per_cu : s->blocks_per_cu);
     HIP_TRY(hipEventRecord(s->ev0, stream));
-    HIP_TRY(launch_path(s->dev, s->camf, p, s->variant, grid, stream, false));
+    HIP_TRY(launch_path(s->dev, s->camf, p, s->variant, grid, stream, s->stats_on));
     HIP_TRY(hipEventRecord(s->ev1, stream));
     return RT_OK;
 }
@@ -578,6 +601,41 @@ int rt_last_kernel_ms(rt_scene* s, float* ms)
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipEventSynchronize(s->ev1));
     HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
+    return RT_OK;
+}
+
+int rt_scene_set_stats(rt_scene* s, int32_t enable)
+{
+    if (!s) {
+        set_error("rt_scene_set_stats: null scene");
+        return RT_ERR_ARG;
+    }
+    HIP_TRY(hipSetDevice(s->device));
+    if (enable) {
+        HIP_TRY(s->stats_buf.reserve(RT_STATS_COUNT));
+        HIP_TRY(hipMemset(s->stats_buf.p, 0, RT_STATS_COUNT * sizeof(unsigned long long)));
+        s->stats_blocks_per_cu = path_blocks_per_cu(s->variant, path_lds_bytes(s->dev), true);
+    }
+    s->stats_on = enable != 0;
+    return RT_OK;
+}
+
+int rt_scene_get_stats(rt_scene* s, uint64_t* out, int32_t n)
+{
+    if (!s || !out || n < 0) {
+        set_error("rt_scene_get_stats: bad argument");
+        return RT_ERR_ARG;
+    }
+    if (!s->stats_buf.p) {
+        set_error("rt_scene_get_stats: statistics were never enabled");
+        return RT_ERR_STATE;
+    }
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned long long v[RT_STATS_COUNT];
+    HIP_TRY(hipMemcpy(v, s->stats_buf.p, sizeof v, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(s->stats_buf.p, 0, sizeof v));
+    for (int k = 0; k < n && k < RT_STATS_COUNT; k++) out[k] = v[k];
     return RT_OK;
 }
 
