@@ -221,7 +221,7 @@ def main() -> int:
                                  f"(SURVEY B_ray {bpr:.0f} B/ray, scene served on chip): "
                                  f"{bpr * my_rays_per_step / (avg_ms * 1e-3) / 1e9:.0f} GB/s"},
             "path_stats": {"per_ray": {k: round(st[k], 3) for k in ("nodes", "tris", "sphs")},
-                           "wave_cycle_split": st["cycles"], "wave_iters_per_ray": st["wave_iters_per_ray"]},
+                           "lane_slots_per_ray": st["wave_iters_per_ray"]},
         }
         if not args.no_cpu_baseline and world == 1:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)

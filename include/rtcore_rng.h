@@ -12,8 +12,9 @@
  *           pixel  = y * frame_width + x   (whole-frame index, independent of tiling)
  *           sample = sample_base + s       (the s-th sample rendered for this pixel)
  *   draw n (n = 0, 1, 2, ...):
- *           h = lowbias32( lowbias32(lo32(key) + n * 0x9E3779B9) ^ hi32(key) )
+ *           h = lowbias32( (lo32(key) + n * 0x9E3779B9) ^ hi32(key) )    (mod 2^32)
  *           U = (h >> 8) * 2^-24            in [0, 1 - 2^-24]
+ *   i.e. one hash round of a Weyl sequence whose offset and mask are the per-sample key.
  * U has 24 significant bits, so it is exact in float and in double: the fp32 kernel
  * and the fp64 oracle see bit-identical uniforms.  Draws are consumed in the
  * reference's order: camera subX, subY, [dof radius, angle],
@@ -55,8 +56,8 @@ RT_HD uint32_t rt_lowbias32(uint32_t x)
 }
 
 typedef struct rt_rng {
-    uint32_t k0, k1; /* per-sample key */
-    uint32_t n;      /* next draw index */
+    uint32_t k0; /* lo32(key) + n * 0x9E3779B9 for the next draw n */
+    uint32_t k1; /* hi32(key) */
 } rt_rng;
 
 /* The key factors as seed_key = splitmix64(seed), pixel_key = splitmix64(seed_key + pixel),
@@ -69,7 +70,6 @@ RT_HD rt_rng rt_rng_from_pixel_key(uint64_t pixel_key, uint64_t sample)
     rt_rng r;
     r.k0 = (uint32_t)k;
     r.k1 = (uint32_t)(k >> 32);
-    r.n = 0;
     return r;
 }
 
@@ -86,8 +86,8 @@ RT_HD rt_rng rt_rng_init(uint64_t seed, uint64_t pixel, uint64_t sample)
 /* 24-bit draw as an integer in [0, 2^24). */
 RT_HD uint32_t rt_rng_next24(rt_rng* r)
 {
-    uint32_t h = rt_lowbias32(rt_lowbias32(r->k0 + r->n * 0x9E3779B9u) ^ r->k1);
-    r->n += 1;
+    uint32_t h = rt_lowbias32(r->k0 ^ r->k1);
+    r->k0 += 0x9E3779B9u;
     return h >> 8;
 }
 

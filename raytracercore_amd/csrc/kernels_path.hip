@@ -301,15 +301,37 @@ __device__ __forceinline__ float next_u(rt_rng& r) { return rt_rng_next_float(&r
 
 // Vec4D.CreateHorizon(pole, z, theta) (Vec4D.cs:52-58) as the equivalent Rodrigues form:
 // pole*z + (c*cos(theta) + (pole x c)*sin(theta)) * s, c = normalize(pole x z^) or x^.
-__device__ __forceinline__ V3 horizon(V3 pole, float z, float s, float turn)
+// The frame (c, pole x c) depends on the pole only, so one bounce builds it once for both
+// the rough normal and the diffuse direction (both turn about the hit normal).
+struct Frame {
+    V3 c, bn;
+};
+__device__ __forceinline__ Frame make_frame(V3 pole)
 {
     V3 c = v3(pole.y, -pole.x, 0.0f);
     const float cl = fmaf(c.x, c.x, c.y * c.y);
     c = (cl == 0.0f) ? v3(1.0f, 0.0f, 0.0f) : c * __builtin_amdgcn_rsqf(cl);
-    const V3 bn = cross(pole, c);
+    return Frame{c, cross(pole, c)};
+}
+__device__ __forceinline__ V3 horizon(const Frame& f, V3 pole, float z, float s, float turn)
+{
     const float cs = __builtin_amdgcn_cosf(turn), sn = __builtin_amdgcn_sinf(turn); // argument in turns
-    const V3 h = madd(c, cs, bn * sn);
+    const V3 h = madd(f.c, cs, f.bn * sn);
     return madd(h, s, pole * z);
+}
+
+// 2 * acos(u) / pi for u in [0, 1): sqrt(1 - u) * P(u), the degree-7 fit of Abramowitz &
+// Stegun 4.4.46 (|error| <= 2e-8 rad) scaled by 2 / pi; as accurate as fp32 acosf here.
+__device__ __forceinline__ float acos_turn2(float u)
+{
+    float p = fmaf(u, -0.0008037268f, 0.0042463113f);
+    p = fmaf(u, p, -0.0108786384f);
+    p = fmaf(u, p, 0.0196663830f);
+    p = fmaf(u, p, -0.0319419540f);
+    p = fmaf(u, p, 0.0566457845f);
+    p = fmaf(u, p, -0.1366178393f);
+    p = fmaf(u, p, 1.0f);
+    return fsqrt(1.0f - u) * p;
 }
 
 __device__ __forceinline__ void camera_ray(const CameraF& c, float x, float y, V3& o, V3& d)
@@ -432,7 +454,8 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
         z = __builtin_amdgcn_exp2f(a);
         sz = fsqrt(one_minus_exp2_2a(a));
     }
-    const V3 rough = horizon(nrm, z, sz, next_u(S.rng));
+    const Frame fr = make_frame(nrm);
+    const V3 rough = horizon(fr, nrm, z, sz, next_u(S.rng));
 
     const float diff_lum = M.diffuse.w, emis_lum = M.emission.w;
     float spec_lum = M.specular.w, refr_lum = M.refraction.w;
@@ -475,9 +498,9 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
         }
         new_tint = xyz(M.specular);
     } else if (diff_lum != 0.0f && (ray_rand -= diff_lum) <= 0.0f) { // diffuse
-        const float dz = 2.0f * acosf(next_u(S.rng)) * 0.31830988618379067f;
+        const float dz = acos_turn2(next_u(S.rng)); // 2 acos(U) / pi (Raytracer.cs:215)
         const float ds = fsqrt(fmaxf(0.0f, 1.0f - dz * dz));
-        out_dir = horizon(nrm, dz, ds, next_u(S.rng));
+        out_dir = horizon(fr, nrm, dz, ds, next_u(S.rng));
         new_tint = xyz(M.diffuse);
     } else { // emission
         col = S.tint * emis;
@@ -493,7 +516,7 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
 
 // TRAV: RT_TRAVERSAL_BRUTE, or RT_TRAVERSAL_BVH with an LDS stack of STACK entries per lane.
 #ifndef RT_PATH_WAVES
-#define RT_PATH_WAVES 4 // minimum waves per SIMD the register allocator must allow
+#define RT_PATH_WAVES 6 // minimum waves per SIMD the register allocator must allow
 #endif
 // LDS: stage the shading records (PrimF per slot, MatF per ID, XformF) in LDS so that the
 // per-lane gathers after each closest-hit query are LDS reads instead of dependent global loads.

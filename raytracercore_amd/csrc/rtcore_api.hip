@@ -402,7 +402,7 @@ PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint6
     p.spp = spp;
     // a few chunks per pixel keep the tail of a launch short while each lane still amortises
     // its item fetch over many samples (RTCORE_PATH_CHUNKS overrides the count, for tuning)
-    int chunks = 8;
+    int chunks = 32;
     if (const char* e = getenv("RTCORE_PATH_CHUNKS")) chunks = std::max(1, atoi(e));
     p.chunk = std::max(1, std::min(64, (spp + chunks - 1) / chunks));
     p.n_chunks = (spp + p.chunk - 1) / p.chunk;

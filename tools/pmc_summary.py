@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes of the path kernel: per-dispatch counters of the timed
+(non-instrumented) launches and derived ratios.  usage: tools/pmc_summary.py DIR [kernel-substring]"""
+import collections
+import csv
+import glob
+import os
+import sys
+
+d = sys.argv[1]
+sub = sys.argv[2] if len(sys.argv) > 2 else "path_kernel<"
+agg = collections.defaultdict(lambda: collections.defaultdict(float))
+names = {}
+for f in glob.glob(os.path.join(d, "pmc*", "pmc_counter_collection.csv")):
+    for r in csv.DictReader(open(f)):
+        kname = r["Kernel_Name"]
+        tmpl = kname[kname.find("path_kernel<"):].split(">")[0]
+        if sub in kname and not tmpl.endswith("true"):  # skip the instrumented (STATS) variant
+            key = (os.path.basename(os.path.dirname(f)), int(r["Dispatch_Id"]))
+            agg[key][r["Counter_Name"]] += float(r["Counter_Value"])
+            names[key] = r["Kernel_Name"][:70]
+by_pass = collections.defaultdict(list)
+for (p, disp), v in sorted(agg.items()):
+    by_pass[p].append(v)
+tot = {}
+for p, lst in by_pass.items():
+    last = lst[-1]  # the last timed dispatch of that pass
+    tot.update(last)
+for k in sorted(tot):
+    print(f"{k:24s} {tot[k]:.6g}")
+if "SQ_INSTS_VALU" in tot and "SQ_WAVES" in tot:
+    print("VALU instr per wave", tot["SQ_INSTS_VALU"] / tot["SQ_WAVES"])
+    print("SALU/VALU", tot["SQ_INSTS_SALU"] / tot["SQ_INSTS_VALU"])
+if "GRBM_GUI_ACTIVE" in tot and "SQ_INSTS_VALU" in tot:
+    simd_cycles = tot["GRBM_GUI_ACTIVE"] * 1024  # 256 CUs x 4 SIMDs
+    print("VALU busy (4 cyc/instr)", 4 * tot["SQ_INSTS_VALU"] / simd_cycles)
