@@ -223,6 +223,9 @@ def main() -> int:
             "path_stats": {"per_ray": {k: round(st[k], 3) for k in ("nodes", "tris", "sphs")},
                            "lane_slots_per_ray": st["wave_iters_per_ray"]},
         }
+        traffic_file = os.path.join(ROOT, "profiles", "traffic", f"{args.config}.json")
+        if os.path.exists(traffic_file) and args.spp == 0:  # PMC bytes of this launch shape (tools/profile.sh)
+            out["roofline"]["traffic"] = json.load(open(traffic_file))["traffic_bytes"]
         if not args.no_cpu_baseline and world == 1:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
             out["cpu_baseline"] = cpu_baseline(args.config, threads)

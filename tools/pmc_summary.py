@@ -7,8 +7,11 @@ import glob
 import os
 import sys
 
+import json
+
 d = sys.argv[1]
-sub = sys.argv[2] if len(sys.argv) > 2 else "path_kernel<"
+sub = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].endswith(".json") else "path_kernel<"
+json_out = next((a for a in sys.argv[2:] if a.endswith(".json")), None)
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 names = {}
 for f in glob.glob(os.path.join(d, "pmc*", "pmc_counter_collection.csv")):
@@ -34,3 +37,10 @@ if "SQ_INSTS_VALU" in tot and "SQ_WAVES" in tot:
 if "GRBM_GUI_ACTIVE" in tot and "SQ_INSTS_VALU" in tot:
     simd_cycles = tot["GRBM_GUI_ACTIVE"] * 1024  # 256 CUs x 4 SIMDs
     print("VALU busy (4 cyc/instr)", 4 * tot["SQ_INSTS_VALU"] / simd_cycles)
+if json_out and "FETCH_SIZE" in tot and "WRITE_SIZE" in tot:
+    # rocprofv3 reports kB; on gfx950 FETCH_SIZE counts half the bytes of wide reads (MI355X_MICROARCH.md, HBM)
+    rec = {"fetch_size_kb": tot["FETCH_SIZE"], "write_size_kb": tot["WRITE_SIZE"],
+           "traffic_bytes": 2 * tot["FETCH_SIZE"] * 1024 + tot["WRITE_SIZE"] * 1024,
+           "note": "per path-kernel launch; FETCH_SIZE doubled per the gfx950 correction", "source": d}
+    json.dump(rec, open(json_out, "w"), indent=1)
+    print("wrote", json_out, rec["traffic_bytes"])

@@ -12,4 +12,6 @@ rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- p
 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY --output-format csv -d "$out/pmc1" -o pmc -- python3 bench.py --no-cpu-baseline "$@" > "$out/pmc1.log" 2>&1
 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/pmc2" -o pmc -- python3 bench.py --no-cpu-baseline "$@" > "$out/pmc2.log" 2>&1
 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format csv -d "$out/pmc3" -o pmc -- python3 bench.py --no-cpu-baseline "$@" > "$out/pmc3.log" 2>&1
+rocprofv3 --pmc SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_INSTS_VALU_CVT --output-format csv -d "$out/pmc4" -o pmc -- python3 bench.py --no-cpu-baseline "$@" > "$out/pmc4.log" 2>&1
+rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_WAIT_ANY SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_FLOPS_FP32 SQ_LDS_BANK_CONFLICT --output-format csv -d "$out/pmc5" -o pmc -- python3 bench.py --no-cpu-baseline "$@" > "$out/pmc5.log" 2>&1
 echo "profile $tag done"
