@@ -28,7 +28,17 @@ CONFIGS = {
     "bounce1080": ("bounce.txt", 0, 1920, 1080, 256),
     "die1080": ("die.txt", 0, 1920, 1080, 1024),
     "bounce256": ("bounce.txt", 0, 256, 256, 16),
+    # C4: procedural 1M-triangle height field in the bounce room (raytracercore_amd/scenes.py)
+    "mesh1080": ("@mesh", 0, 1920, 1080, 64),
 }
+
+
+def load_scene(rc, scene_file):
+    if scene_file == "@mesh":
+        from raytracercore_amd.scenes import mesh_scene_text
+
+        return rc.SceneLoader.from_text(mesh_scene_text())
+    return rc.SceneLoader.from_file(rc.scene_path(scene_file))
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 vector = fp32 MFMA dense peak
 
 
@@ -78,10 +88,16 @@ def cpu_baseline(cfg_name: str, threads: int):
     import raytracercore_amd as rc
 
     scene_file, cam, W, H, _ = CONFIGS[cfg_name]
-    orc = OracleScene.from_file(rc.scene_path(scene_file))
+    if scene_file == "@mesh":  # 1M triangles: the reference's collect-all-leaves query is slow, so
+        from raytracercore_amd.scenes import mesh_scene_text  # a half-size frame at 1 spp
+
+        orc = OracleScene.from_text(mesh_scene_text())
+        W, H, spp = W // 2, H // 2, 1
+    else:
+        orc = OracleScene.from_file(rc.scene_path(scene_file))
+        spp = 16 if W * H > 100000 else 64  # a few seconds on 16 host threads
     orc.set_size(W, H)
     orc.select_camera(cam)
-    spp = 16 if W * H > 100000 else 64  # a few seconds on 16 host threads
     _, n, m, rays, secs, used = orc.render_frame(spp, seed=0, threads=threads)
     return {
         "value": round(rays / secs / 1e6, 3),
@@ -124,7 +140,7 @@ def main() -> int:
     scene_file, cam, W, H, spp = CONFIGS[args.config]
     if args.spp > 0:
         spp = args.spp
-    scene = rc.SceneLoader.from_file(rc.scene_path(scene_file))
+    scene = load_scene(rc, scene_file)
     trav = {"auto": rc.RT_TRAVERSAL_AUTO, "brute": rc.RT_TRAVERSAL_BRUTE, "bvh": rc.RT_TRAVERSAL_BVH}[args.traversal]
     gpu = rc.GpuRaytracer(scene, cam, device=local, size=(W, H), traversal=trav)
     info = gpu.info()

@@ -242,54 +242,6 @@ __device__ __forceinline__ void divmod(unsigned x, unsigned d, float inv_d, unsi
     }
 }
 
-template <int STACK, bool STATS>
-__device__ __forceinline__ void trace_bvh(const PathScene& s, const NodeF* __restrict__ nodes,
-                                          const TestRec* __restrict__ tests, const XformF* __restrict__ xf, V3 o, V3 d,
-                                          int prev, Best& b, int* stk, Counters& cnt)
-{
-    const V3 id = v3(rcp(d.x), rcp(d.y), rcp(d.z));
-    const V3 oi = o * id;
-    int ref = s.root;
-    int sp = 0;
-    while (true) {
-        if (ref >= 0) {
-            const NodeF n = nodes[ref];
-            if (STATS) cnt.nodes++;
-            float tl, tr;
-            const bool hl = slab(n.lmin, n.lmax, oi, id, b.t, tl);
-            const bool hr = slab(n.rmin, n.rmax, oi, id, b.t, tr);
-            const int cl = __float_as_int(n.lmin.w), cr = __float_as_int(n.rmin.w);
-            if (hl && hr) {
-                const bool lf = tl <= tr;
-                if (sp < STACK) stk[(sp++) * 256] = lf ? cr : cl; // host guarantees depth < STACK
-                ref = lf ? cl : cr;
-                continue;
-            }
-            if (hl) {
-                ref = cl;
-                continue;
-            }
-            if (hr) {
-                ref = cr;
-                continue;
-            }
-        } else {
-            const int code = ~ref;
-            const int first = code >> 3, c = (code & 7) + 1;
-            for (int k = first; k < first + c; k++) {
-                const TestRec R = tests[k];
-                if (STATS) {
-                    if ((__float_as_uint(R.meta.y) & KIND_MASK) == RT_PRIM_TRIANGLE) cnt.tris++;
-                    else cnt.sphs++;
-                }
-                hit_any(R, k, o, d, prev, xf, b);
-            }
-        }
-        if (sp == 0) break;
-        ref = stk[(--sp) * 256];
-    }
-}
-
 struct Sample {
     V3 o, d, tint;
     int bounce;
@@ -334,18 +286,23 @@ __device__ __forceinline__ float acos_turn2(float u)
     return fsqrt(1.0f - u) * p;
 }
 
-__device__ __forceinline__ void camera_ray(const CameraF& c, float x, float y, V3& o, V3& d)
+struct Ray3 {
+    V3 o, d;
+};
+__device__ __forceinline__ Ray3 camera_ray(const CameraF& c, float x, float y)
 {
+    Ray3 r;
     if (c.kind == RT_CAMERA_FRUSTUM) {
         const float ox = c.tan_x * ((x - c.w2) * rcp(c.w2));
         const float oy = c.tan_y * ((y - c.h2) * rcp(c.h2));
-        d = normalize(madd(xyz(c.up), oy, madd(xyz(c.side), ox, xyz(c.look))));
-        o = xyz(c.position);
+        r.d = normalize(madd(xyz(c.up), oy, madd(xyz(c.side), ox, xyz(c.look))));
+        r.o = xyz(c.position);
     } else {
-        o = madd(xyz(c.up), (y - c.h2) * c.v_mult, madd(xyz(c.side), (x - c.w2) * c.h_mult, xyz(c.position)));
-        d = normalize(xyz(c.look));
+        r.o = madd(xyz(c.up), (y - c.h2) * c.v_mult, madd(xyz(c.side), (x - c.w2) * c.h_mult, xyz(c.position)));
+        r.d = normalize(xyz(c.look));
     }
-    o = madd(d, c.image_plane, o);
+    r.o = madd(r.d, c.image_plane, r.o);
+    return r;
 }
 
 // Raytracer.GetCameraRay (Raytracer.cs:262-282)
@@ -353,16 +310,17 @@ __device__ __forceinline__ void start_sample(const CameraF& cam, int x, int y, S
 {
     const float sx = (float)x + next_u(S.rng);
     const float sy = (float)y + next_u(S.rng);
-    camera_ray(cam, sx, sy, S.o, S.d);
+    const Ray3 r = camera_ray(cam, sx, sy);
+    S.o = r.o;
+    S.d = r.d;
     if (cam.dof != 0.0f) {
-        const V3 focus = madd(S.d, cam.focal_length - cam.image_plane, S.o);
+        const V3 focus = madd(r.d, cam.focal_length - cam.image_plane, r.o);
         const float dist = fsqrt(next_u(S.rng)) * cam.dof;
         const float turn = next_u(S.rng);
         const float ox = __builtin_amdgcn_cosf(turn) * dist, oy = __builtin_amdgcn_sinf(turn) * dist;
-        V3 o2, d2;
-        camera_ray(cam, sx + ox, sy + oy, o2, d2);
-        S.o = o2;
-        S.d = normalize(focus - o2);
+        const Ray3 r2 = camera_ray(cam, sx + ox, sy + oy);
+        S.o = r2.o;
+        S.d = normalize(focus - r2.o);
     }
     S.tint = v3(1.0f, 1.0f, 1.0f);
     S.bounce = 0;
@@ -514,149 +472,143 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
     return 0;
 }
 
-// TRAV: RT_TRAVERSAL_BRUTE, or RT_TRAVERSAL_BVH with an LDS stack of STACK entries per lane.
 #ifndef RT_PATH_WAVES
-#define RT_PATH_WAVES 6 // minimum waves per SIMD the register allocator must allow
+#define RT_PATH_WAVES 6 // minimum waves per SIMD the register allocator must allow (brute force)
 #endif
-// LDS: stage the shading records (PrimF per slot, MatF per ID, XformF) in LDS so that the
-// per-lane gathers after each closest-hit query are LDS reads instead of dependent global loads.
-template <int TRAV, int STACK, bool LDS, bool STATS>
-__global__ void __launch_bounds__(256, RT_PATH_WAVES)
-    path_kernel(PathScene s, CameraF cam, PathParams p, const TestRec* __restrict__ tests,
-                const RectRec* __restrict__ rects, const PrimF* __restrict__ prims_g, const NodeF* __restrict__ nodes,
-                const XformF* __restrict__ xf, const MatF* __restrict__ mats_g, const float4* __restrict__ vnormals)
+#ifndef RT_BVH_WAVES
+#define RT_BVH_WAVES 4 // the same for the BVH kernel (its LDS stack caps occupancy anyway)
+#endif
+
+// LDS staging of the shading records (PrimF per slot, MatF per ID, XformF): the per-lane gathers
+// after each closest-hit query become LDS reads instead of dependent global loads.
+struct ShadeRecs {
+    const PrimF* prims;
+    const MatF* mats;
+    const XformF* xfs;
+};
+template <bool LDS>
+__device__ __forceinline__ ShadeRecs stage_scene(const PathScene& s, const PrimF* prims_g, const MatF* mats_g,
+                                                 const XformF* xf, float4* lds_scene)
 {
-    __shared__ int stack_mem[TRAV == RT_TRAVERSAL_BVH ? STACK * 256 : 1];
-    extern __shared__ float4 lds_scene[];
-    int* stk = stack_mem + threadIdx.x;
-    const PrimF* __restrict__ prims = prims_g;
-    const MatF* __restrict__ mats = mats_g;
-    const XformF* __restrict__ xfs = xf;
-    if (LDS) {
-        const int n_p = s.n_slots * 4, n_m = s.n_ids * 5, n_x = s.n_xf * 9;
-        const float4* gp = reinterpret_cast<const float4*>(prims_g);
-        const float4* gm = reinterpret_cast<const float4*>(mats_g);
-        const float4* gx = reinterpret_cast<const float4*>(xf);
-        for (int i = threadIdx.x; i < n_p; i += 256) lds_scene[i] = gp[i];
-        for (int i = threadIdx.x; i < n_m; i += 256) lds_scene[n_p + i] = gm[i];
-        for (int i = threadIdx.x; i < n_x; i += 256) lds_scene[n_p + n_m + i] = gx[i];
-        __syncthreads();
-        prims = reinterpret_cast<const PrimF*>(lds_scene);
-        mats = reinterpret_cast<const MatF*>(lds_scene + n_p);
-        xfs = reinterpret_cast<const XformF*>(lds_scene + n_p + n_m);
+    if (!LDS) return ShadeRecs{prims_g, mats_g, xf};
+    const int n_p = s.n_slots * 4, n_m = s.n_ids * 5, n_x = s.n_xf * 9;
+    const float4* gp = reinterpret_cast<const float4*>(prims_g);
+    const float4* gm = reinterpret_cast<const float4*>(mats_g);
+    const float4* gx = reinterpret_cast<const float4*>(xf);
+    for (int i = threadIdx.x; i < n_p; i += blockDim.x) lds_scene[i] = gp[i];
+    for (int i = threadIdx.x; i < n_m; i += blockDim.x) lds_scene[n_p + i] = gm[i];
+    for (int i = threadIdx.x; i < n_x; i += blockDim.x) lds_scene[n_p + n_m + i] = gx[i];
+    __syncthreads();
+    return ShadeRecs{reinterpret_cast<const PrimF*>(lds_scene), reinterpret_cast<const MatF*>(lds_scene + n_p),
+                     reinterpret_cast<const XformF*>(lds_scene + n_p + n_m)};
+}
+
+// One lane's work: the open work item (a chunk of samples of one pixel), its running sums and
+// the sample in flight.  The wave's item pool [pool_next, pool_end) is wave-uniform.
+struct Lane {
+    bool active, item_open, live;
+    unsigned item;
+    int fx, fy, s_next, s_end;
+    unsigned long long pkey; // rt_rng_pixel_key of the open item's pixel
+    float ar, ag, ab;
+    unsigned n_s, n_m, rays;
+    unsigned pool_next, pool_end;
+};
+
+__device__ __forceinline__ void lane_init(Lane& L)
+{
+    L.active = true;
+    L.item_open = L.live = false;
+    L.item = 0;
+    L.fx = L.fy = L.s_next = L.s_end = 0;
+    L.pkey = 0;
+    L.ar = L.ag = L.ab = 0.0f;
+    L.n_s = L.n_m = L.rays = 0;
+    L.pool_next = L.pool_end = 0;
+}
+
+// Lanes without a sample in flight close finished items and take new ones from the wave's
+// pool (one atomic per 64 items), then start the next camera sample of their item.
+__device__ __forceinline__ void refill(Lane& L, Sample& S, const PathParams& p, const PathScene& s, const CameraF& cam, int lane,
+                                      unsigned total)
+{
+    const bool need = L.active && !L.live && (!L.item_open || L.s_next >= L.s_end);
+    if (need && L.item_open) {
+        p.partial[L.item] = make_float4(L.ar, L.ag, L.ab, __uint_as_float(L.n_s | (L.n_m << 16)));
+        L.item_open = false;
     }
-    const int lane = threadIdx.x & 63;
-    const unsigned total = (unsigned)p.n_chunks * (unsigned)p.n_pad;
-    const int pln0 = s.n_bvh;
-
-    bool active = true, item_open = false, live = false;
-    unsigned item = 0;
-    int fx = 0, fy = 0, s_next = 0, s_end = 0;
-    unsigned long long pkey = 0; // rt_rng_pixel_key of the open item's pixel
-    float ar = 0.0f, ag = 0.0f, ab = 0.0f;
-    unsigned n_s = 0, n_m = 0, rays = 0;
-    // the wave's pool of work items: [pool_next, pool_end), refilled 64 at a time
-    unsigned pool_next = 0, pool_end = 0;
-    Counters cnt{};
-    Sample S;
-    S.prev = -1;
-    S.bounce = 0;
-
-    while (true) {
-        unsigned long long t0 = 0, t1 = 0, t2 = 0;
-        if (STATS) t0 = __builtin_readcyclecounter();
-        const bool need = active && !live && (!item_open || s_next >= s_end);
-        if (need && item_open) {
-            p.partial[item] = make_float4(ar, ag, ab, __uint_as_float(n_s | (n_m << 16)));
-            item_open = false;
+    const unsigned long long m = __ballot(need);
+    if (m) {
+        const unsigned k = (unsigned)__popcll(m), avail = L.pool_end - L.pool_next;
+        unsigned fresh = 0;
+        if (k > avail) { // wave-uniform: one atomic refills the pool
+            if (lane == 0) fresh = atomicAdd(p.counter, 64u);
+            fresh = __builtin_amdgcn_readfirstlane(fresh);
         }
-        const unsigned long long m = __ballot(need);
-        if (m) {
-            const unsigned k = (unsigned)__popcll(m), avail = pool_end - pool_next;
-            unsigned fresh = 0;
-            if (k > avail) { // wave-uniform: one atomic refills the pool
-                if (lane == 0) fresh = atomicAdd(p.counter, 64u);
-                fresh = __builtin_amdgcn_readfirstlane(fresh);
-            }
-            if (need) {
-                const unsigned r = (unsigned)__popcll(m & ((1ull << lane) - 1ull));
-                item = r < avail ? pool_next + r : fresh + (r - avail);
-                if (item >= total) {
-                    active = false;
-                } else {
-                    unsigned c, q, by, bx;
-                    divmod(item, (unsigned)p.n_pad, p.inv_n_pad, c, q);
-                    divmod(q >> 6, (unsigned)p.blocks_x, p.inv_blocks_x, by, bx);
-                    const int px = (int)bx * 8 + (q & 7), py = (int)by * 8 + ((q >> 3) & 7);
-                    if (px < p.w && py < p.h) {
-                        item_open = true;
-                        s_next = (int)c * p.chunk;
-                        s_end = min(p.spp, s_next + p.chunk);
-                        ar = ag = ab = 0.0f;
-                        n_s = n_m = 0;
-                        fx = p.x0 + px;
-                        fy = p.band > 0 ? p.y0 + ((py / p.band) * p.band_stride + p.band_offset) * p.band + py % p.band
-                                        : p.y0 + py;
-                        pkey = rt_rng_pixel_key(p.seed_key, (unsigned long long)fy * (unsigned long long)s.width +
-                                                                (unsigned long long)fx);
-                    }
-                }
-            }
-            if (k > avail) {
-                pool_next = fresh + (k - avail);
-                pool_end = fresh + 64u;
+        if (need) {
+            const unsigned r = (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+            L.item = r < avail ? L.pool_next + r : fresh + (r - avail);
+            if (L.item >= total) {
+                L.active = false;
             } else {
-                pool_next += k;
-            }
-        }
-        if (!__any(active)) break;
-        if (active && item_open && !live && s_next < s_end) {
-            S.rng = rt_rng_from_pixel_key(pkey, p.sample_base + (unsigned long long)s_next);
-            start_sample(cam, fx, fy, S);
-            live = true;
-        }
-        if (STATS) t1 = __builtin_readcyclecounter();
-        if (live) {
-            Best b{__builtin_huge_valf(), -1, 0.0f, 0.0f};
-            if (TRAV == RT_TRAVERSAL_BVH) {
-                trace_bvh<STACK, STATS>(s, nodes, tests, xf, S.o, S.d, S.prev, b, stk, cnt);
-            } else {
-                trace_brute(s, tests, rects, xf, S.o, S.d, S.prev, b);
-                if (STATS) {
-                    cnt.tris += s.n_rect[0] + s.n_rect[1] + s.n_rect[2] + s.n_tri;
-                    cnt.sphs += s.n_sph;
+                unsigned c, q, by, bx;
+                divmod(L.item, (unsigned)p.n_pad, p.inv_n_pad, c, q);
+                divmod(q >> 6, (unsigned)p.blocks_x, p.inv_blocks_x, by, bx);
+                const int px = (int)bx * 8 + (q & 7), py = (int)by * 8 + ((q >> 3) & 7);
+                if (px < p.w && py < p.h) {
+                    L.item_open = true;
+                    L.s_next = (int)c * p.chunk;
+                    L.s_end = min(p.spp, L.s_next + p.chunk);
+                    L.ar = L.ag = L.ab = 0.0f;
+                    L.n_s = L.n_m = 0;
+                    L.fx = p.x0 + px;
+                    L.fy = p.band > 0 ? p.y0 + ((py / p.band) * p.band_stride + p.band_offset) * p.band + py % p.band
+                                      : p.y0 + py;
+                    L.pkey = rt_rng_pixel_key(p.seed_key, (unsigned long long)L.fy * (unsigned long long)s.width +
+                                                              (unsigned long long)L.fx);
                 }
             }
-            for (int i = pln0; i < pln0 + s.n_pln; i++) hit_plane(tests[i], i, S.o, S.d, S.prev, b);
-            rays++;
-            if (STATS) t2 = __builtin_readcyclecounter();
-            V3 col;
-            const int r = shade(s, prims, mats, xfs, vnormals, b, S, col);
-            if (r != 0) {
-                if (r == 1) {
-                    ar += col.x;
-                    ag += col.y;
-                    ab += col.z;
-                    n_s++;
-                } else {
-                    n_m++;
-                }
-                s_next++;
-                live = false;
-            }
-        } else if (STATS) {
-            t2 = __builtin_readcyclecounter();
         }
-        if (STATS) {
-            const unsigned long long t3 = __builtin_readcyclecounter();
-            cnt.cyc_start += t1 - t0;
-            cnt.cyc_trace += t2 - t1;
-            cnt.cyc_shade += t3 - t2;
-            cnt.iters++;
+        if (k > avail) {
+            L.pool_next = fresh + (k - avail);
+            L.pool_end = fresh + 64u;
+        } else {
+            L.pool_next += k;
         }
     }
+    if (L.active && L.item_open && !L.live && L.s_next < L.s_end) {
+        S.rng = rt_rng_from_pixel_key(L.pkey, p.sample_base + (unsigned long long)L.s_next);
+        start_sample(cam, L.fx, L.fy, S);
+        L.live = true;
+    }
+}
+
+// After a closest-hit query: one bounce of GetColor; a finished sample goes into the item's sums.
+__device__ __forceinline__ void bounce(Lane& L, Sample& S, const PathScene& s, const ShadeRecs& R, const float4* vnormals,
+                                       const Best& b)
+{
+    L.rays++;
+    V3 col;
+    const int r = shade(s, R.prims, R.mats, R.xfs, vnormals, b, S, col);
+    if (r != 0) {
+        if (r == 1) {
+            L.ar += col.x;
+            L.ag += col.y;
+            L.ab += col.z;
+            L.n_s++;
+        } else {
+            L.n_m++;
+        }
+        L.s_next++;
+        L.live = false;
+    }
+}
+
+template <bool STATS>
+__device__ __forceinline__ void flush_counts(const Lane& L, const Counters& cnt, const PathParams& p, int lane)
+{
     // one 64-bit add per wave for the ray count (and the optional traversal counters)
-    unsigned long long wr = rays;
+    unsigned long long wr = L.rays;
     for (int off = 32; off > 0; off >>= 1) wr += __shfl_down(wr, off);
     if (lane == 0) atomicAdd(p.rays, wr);
     if (STATS) {
@@ -676,6 +628,153 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
             atomicAdd(p.stats + 6, cnt.iters);
         }
     }
+}
+
+// Brute-force megakernel: every loop iteration issues one closest-hit query per live lane
+// (the scene's records arrive through scalar loads) and shades it.
+template <bool LDS, bool STATS>
+__global__ void __launch_bounds__(256, RT_PATH_WAVES)
+    path_kernel(PathScene s, CameraF cam, PathParams p, const TestRec* __restrict__ tests,
+                const RectRec* __restrict__ rects, const PrimF* __restrict__ prims_g, const NodeF* __restrict__ nodes,
+                const XformF* __restrict__ xf, const MatF* __restrict__ mats_g, const float4* __restrict__ vnormals)
+{
+    extern __shared__ float4 lds_scene[];
+    const ShadeRecs R = stage_scene<LDS>(s, prims_g, mats_g, xf, lds_scene);
+    const int lane = threadIdx.x & 63;
+    const unsigned total = (unsigned)p.n_chunks * (unsigned)p.n_pad;
+    const int pln0 = s.n_bvh;
+    Lane L;
+    lane_init(L);
+    Sample S;
+    S.prev = -1;
+    S.bounce = 0;
+    Counters cnt{};
+
+    while (true) {
+        unsigned long long t0 = 0, t1 = 0, t2 = 0;
+        if (STATS) t0 = __builtin_readcyclecounter();
+        refill(L, S, p, s, cam, lane, total);
+        if (!__any(L.active)) break;
+        if (STATS) t1 = __builtin_readcyclecounter();
+        if (L.live) {
+            Best b{__builtin_huge_valf(), -1, 0.0f, 0.0f};
+            trace_brute(s, tests, rects, xf, S.o, S.d, S.prev, b);
+            if (STATS) {
+                cnt.tris += s.n_rect[0] + s.n_rect[1] + s.n_rect[2] + s.n_tri;
+                cnt.sphs += s.n_sph;
+            }
+            for (int i = pln0; i < pln0 + s.n_pln; i++) hit_plane(tests[i], i, S.o, S.d, S.prev, b);
+            if (STATS) t2 = __builtin_readcyclecounter();
+            bounce(L, S, s, R, vnormals, b);
+        } else if (STATS) {
+            t2 = __builtin_readcyclecounter();
+        }
+        if (STATS) {
+            const unsigned long long t3 = __builtin_readcyclecounter();
+            cnt.cyc_start += t1 - t0;
+            cnt.cyc_trace += t2 - t1;
+            cnt.cyc_shade += t3 - t2;
+            cnt.iters++;
+        }
+    }
+    flush_counts<STATS>(L, cnt, p, lane);
+}
+
+// BVH megakernel with decoupled traversal.  A loop iteration advances every traversing lane by
+// one step (one node visit, or one leaf's primitives); lanes whose query finished wait, and
+// the shading / new-sample phase runs only once at least p.refill lanes wait (or none is still
+// traversing).  So one long traversal no longer holds the other 63 lanes of its wave, and the
+// divergent shading code is paid once per batch of finished queries.
+template <int STACK, bool LDS, bool STATS>
+__global__ void __launch_bounds__(256, RT_BVH_WAVES)
+    path_kernel_bvh(PathScene s, CameraF cam, PathParams p, const TestRec* __restrict__ tests,
+                    const RectRec* __restrict__ rects, const PrimF* __restrict__ prims_g,
+                    const NodeF* __restrict__ nodes, const XformF* __restrict__ xf, const MatF* __restrict__ mats_g,
+                    const float4* __restrict__ vnormals)
+{
+    __shared__ int stack_mem[STACK * 256];
+    extern __shared__ float4 lds_scene[];
+    int* stk = stack_mem + threadIdx.x;
+    const ShadeRecs R = stage_scene<LDS>(s, prims_g, mats_g, xf, lds_scene);
+    const int lane = threadIdx.x & 63;
+    const unsigned total = (unsigned)p.n_chunks * (unsigned)p.n_pad;
+    const int pln0 = s.n_bvh;
+    Lane L;
+    lane_init(L);
+    Sample S;
+    S.prev = -1;
+    S.bounce = 0;
+    Counters cnt{};
+    // traversal state of the lane's current query
+    bool trav = false, done = false;
+    int ref = 0, sp = 0;
+    V3 id{0, 0, 0}, oi{0, 0, 0};
+    Best b{__builtin_huge_valf(), -1, 0.0f, 0.0f};
+
+    while (true) {
+        const unsigned long long waiting = __ballot(!trav && (L.active || L.live));
+        const unsigned long long busy = __ballot(trav);
+        if (!waiting && !busy) break;
+        if (!busy || __popcll(waiting) >= p.refill) {
+            if (done) { // the query finished: planes (outside the BVH), then one bounce
+                for (int i = pln0; i < pln0 + s.n_pln; i++) hit_plane(tests[i], i, S.o, S.d, S.prev, b);
+                bounce(L, S, s, R, vnormals, b);
+                done = false;
+            }
+            refill(L, S, p, s, cam, lane, total);
+            if (L.live && !trav) { // start the next query
+                id = v3(rcp(S.d.x), rcp(S.d.y), rcp(S.d.z));
+                oi = S.o * id;
+                ref = s.root;
+                sp = 0;
+                b = Best{__builtin_huge_valf(), -1, 0.0f, 0.0f};
+                trav = true;
+            }
+        }
+        if (trav) { // one traversal step
+            bool pop = true; // child references are node indices or ~leaf codes (any int)
+            if (ref >= 0) {
+                const NodeF n = nodes[ref];
+                if (STATS) cnt.nodes++;
+                float tl, tr;
+                const bool hl = slab(n.lmin, n.lmax, oi, id, b.t, tl);
+                const bool hr = slab(n.rmin, n.rmax, oi, id, b.t, tr);
+                const int cl = __float_as_int(n.lmin.w), cr = __float_as_int(n.rmin.w);
+                if (hl && hr) {
+                    const bool lf = tl <= tr;
+                    if (sp < STACK) stk[(sp++) * 256] = lf ? cr : cl; // host guarantees depth < STACK
+                    ref = lf ? cl : cr;
+                    pop = false;
+                } else if (hl | hr) {
+                    ref = hl ? cl : cr;
+                    pop = false;
+                }
+            } else {
+                const int code = ~ref;
+                const int first = code >> 3, c = (code & 7) + 1;
+                TestRec cur = tests[first];
+                for (int k = first; k < first + c; k++) {
+                    const TestRec nxt = tests[k + 1]; // the record array carries one spare at the end
+                    if (STATS) {
+                        if ((__float_as_uint(cur.meta.y) & KIND_MASK) == RT_PRIM_TRIANGLE) cnt.tris++;
+                        else cnt.sphs++;
+                    }
+                    hit_any(cur, k, S.o, S.d, S.prev, xf, b);
+                    cur = nxt;
+                }
+            }
+            if (pop) {
+                if (sp > 0) {
+                    ref = stk[(--sp) * 256];
+                } else {
+                    trav = false;
+                    done = true;
+                }
+            }
+        }
+        if (STATS) cnt.iters++;
+    }
+    flush_counts<STATS>(L, cnt, p, lane);
 }
 
 __global__ void accumulate_kernel(PathParams p, double* sum, uint32_t* samples, uint32_t* misses)
@@ -720,22 +819,27 @@ __global__ void colors_1spp_kernel(PathParams p, double* out)
 using PathKernel = void (*)(PathScene, CameraF, PathParams, const TestRec*, const RectRec*, const PrimF*,
                             const NodeF*, const XformF*, const MatF*, const float4*);
 
-template <int TRAV, int STACK, bool LDS>
-PathKernel pick_stats(bool stats)
+template <bool LDS>
+PathKernel pick_brute(bool stats)
 {
-    return stats ? path_kernel<TRAV, STACK, LDS, true> : path_kernel<TRAV, STACK, LDS, false>;
+    return stats ? path_kernel<LDS, true> : path_kernel<LDS, false>;
+}
+template <int STACK, bool LDS>
+PathKernel pick_bvh(bool stats)
+{
+    return stats ? path_kernel_bvh<STACK, LDS, true> : path_kernel_bvh<STACK, LDS, false>;
 }
 
 // variant = traversal * 2 + lds; traversal 0 brute force, 1 BVH (24-entry stack), 2 BVH (48)
 PathKernel pick(int variant, bool stats)
 {
     switch (variant) {
-    case 1: return pick_stats<RT_TRAVERSAL_BRUTE, 1, true>(stats);
-    case 2: return pick_stats<RT_TRAVERSAL_BVH, 24, false>(stats);
-    case 3: return pick_stats<RT_TRAVERSAL_BVH, 24, true>(stats);
-    case 4: return pick_stats<RT_TRAVERSAL_BVH, 48, false>(stats);
-    case 5: return pick_stats<RT_TRAVERSAL_BVH, 48, true>(stats);
-    default: return pick_stats<RT_TRAVERSAL_BRUTE, 1, false>(stats);
+    case 1: return pick_brute<true>(stats);
+    case 2: return pick_bvh<24, false>(stats);
+    case 3: return pick_bvh<24, true>(stats);
+    case 4: return pick_bvh<48, false>(stats);
+    case 5: return pick_bvh<48, true>(stats);
+    default: return pick_brute<false>(stats);
     }
 }
 

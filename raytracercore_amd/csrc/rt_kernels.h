@@ -14,6 +14,7 @@ struct PathParams {
     int n_chunks;               // ceil(spp / chunk)
     int blocks_x;               // 8x8 pixel blocks per tile row
     int n_pad;                  // padded pixels per chunk (blocks * 64)
+    int refill;                 // BVH kernel: waiting lanes (of 64) that trigger the shading phase
     float inv_n_pad, inv_blocks_x; // fp32 reciprocals for the item decode
     unsigned long long seed;
     unsigned long long seed_key;   // rt_splitmix64(seed) (rtcore_rng.h)

@@ -409,6 +409,8 @@ PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint6
     p.blocks_x = (w + 7) / 8;
     p.n_pad = p.blocks_x * ((h + 7) / 8) * 64;
     p.inv_n_pad = 1.0f / (float)p.n_pad;
+    p.refill = 16;
+    if (const char* e = getenv("RTCORE_BVH_REFILL")) p.refill = std::max(1, std::min(64, atoi(e)));
     p.inv_blocks_x = 1.0f / (float)p.blocks_x;
     p.seed = seed;
     p.seed_key = rt_splitmix64(seed);

@@ -73,9 +73,19 @@ def _bytes(arr):
     return [bytes(x) for x in arr]
 
 
-@pytest.mark.parametrize("name", ["bounce.txt", "die.txt", "SYNTH"])
+def _scene_text(rc, name):
+    if name == "SYNTH":
+        return SYNTH
+    if name == "MESH":  # config C4's generator at 20 x 10 vertices (342 triangles)
+        from raytracercore_amd.scenes import mesh_scene_text
+
+        return mesh_scene_text(nx=20, ny=10)
+    return open(rc.scene_path(name)).read()
+
+
+@pytest.mark.parametrize("name", ["bounce.txt", "die.txt", "SYNTH", "MESH"])
 def test_loader_matches_oracle(rc, name):
-    text = SYNTH if name == "SYNTH" else open(rc.scene_path(name)).read()
+    text = _scene_text(rc, name)
     ps = rc.SceneLoader.from_text(text)
     orc = OracleScene.from_text(text)
     params, prims, cams = orc.export()
@@ -85,9 +95,9 @@ def test_loader_matches_oracle(rc, name):
     assert _bytes(ps.cameras) == _bytes(cams)
 
 
-@pytest.mark.parametrize("name", ["bounce.txt", "die.txt", "SYNTH"])
+@pytest.mark.parametrize("name", ["bounce.txt", "die.txt", "SYNTH", "MESH"])
 def test_reference_bvh_matches_oracle(rc, name):
-    text = SYNTH if name == "SYNTH" else open(rc.scene_path(name)).read()
+    text = _scene_text(rc, name)
     ps = rc.SceneLoader.from_text(text)
     orc = OracleScene.from_text(text)
     order, boxes, nodes, depth = rc.ref_bvh_export(list(ps.prims))
@@ -145,3 +155,16 @@ def test_loader_ignores_unknown_and_comments(rc):
                                   ((-1, -1, -1), 1, 0, (0, 0, 0), 0, 1)])
 def test_sample_output_matches_oracle(rc, args):
     assert rc.sample_output(*args) == orc_sample_output(*args)
+
+
+def test_mesh_generator_shape(rc):
+    """C4: 1001 x 501 vertices -> 1,000,000 triangles in the bounce room (counted on a small grid)."""
+    from raytracercore_amd.scenes import heightfield_text, mesh_scene_text
+
+    t = heightfield_text(nx=31, ny=11)
+    assert t.count("\nvertex ") == 31 * 11 and t.count("\ntri ") == 2 * 30 * 10
+    ps = rc.SceneLoader.from_text(mesh_scene_text(nx=31, ny=11))
+    room = rc.SceneLoader.from_text(mesh_scene_text(nx=2, ny=2))
+    assert ps.n_prims - room.n_prims == 2 * 30 * 10 - 2
+    zs = np.array([[p.p[k].z for k in range(3)] for p in list(ps.prims)[room.n_prims:]])
+    assert zs.min() > -0.47 and zs.max() < -0.13  # -0.3 +- (0.15 + 0.01)

@@ -10,14 +10,15 @@ import sys
 import json
 
 d = sys.argv[1]
-sub = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].endswith(".json") else "path_kernel<"
+sub = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].endswith(".json") else "path_kernel"
 json_out = next((a for a in sys.argv[2:] if a.endswith(".json")), None)
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 names = {}
 for f in glob.glob(os.path.join(d, "pmc*", "pmc_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         kname = r["Kernel_Name"]
-        tmpl = kname[kname.find("path_kernel<"):].split(">")[0]
+        i = kname.find("path_kernel")
+        tmpl = kname[i:].split(">")[0] if i >= 0 else ""
         if sub in kname and not tmpl.endswith("true"):  # skip the instrumented (STATS) variant
             key = (os.path.basename(os.path.dirname(f)), int(r["Dispatch_Id"]))
             agg[key][r["Counter_Name"]] += float(r["Counter_Value"])
