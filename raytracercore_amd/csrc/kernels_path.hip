@@ -476,7 +476,7 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
 #define RT_PATH_WAVES 6 // minimum waves per SIMD the register allocator must allow (brute force)
 #endif
 #ifndef RT_BVH_WAVES
-#define RT_BVH_WAVES 4 // the same for the BVH kernel (its LDS stack caps occupancy anyway)
+#define RT_BVH_WAVES 5 // the same for the BVH kernel (its LDS stack caps occupancy anyway)
 #endif
 
 // LDS staging of the shading records (PrimF per slot, MatF per ID, XformF): the per-lane gathers
@@ -707,7 +707,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
     Counters cnt{};
     // traversal state of the lane's current query
     bool trav = false, done = false;
-    int ref = 0, sp = 0;
+    int ref = 0, sp = 0, k = 0, kend = 0; // [k, kend): primitives of the leaf being tested
     V3 id{0, 0, 0}, oi{0, 0, 0};
     Best b{__builtin_huge_valf(), -1, 0.0f, 0.0f};
 
@@ -727,13 +727,26 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                 oi = S.o * id;
                 ref = s.root;
                 sp = 0;
+                k = kend = 0;
+                if (ref < 0) { // the root itself is a leaf
+                    k = (~ref) >> 3;
+                    kend = k + ((~ref) & 7) + 1;
+                }
                 b = Best{__builtin_huge_valf(), -1, 0.0f, 0.0f};
                 trav = true;
             }
         }
-        if (trav) { // one traversal step
+        if (trav) { // one traversal step: one node visit, or one primitive of the current leaf
             bool pop = true; // child references are node indices or ~leaf codes (any int)
-            if (ref >= 0) {
+            if (k < kend) {
+                const TestRec rec = tests[k];
+                if (STATS) {
+                    if ((__float_as_uint(rec.meta.y) & KIND_MASK) == RT_PRIM_TRIANGLE) cnt.tris++;
+                    else cnt.sphs++;
+                }
+                hit_any(rec, k, S.o, S.d, S.prev, xf, b);
+                pop = ++k >= kend;
+            } else {
                 const NodeF n = nodes[ref];
                 if (STATS) cnt.nodes++;
                 float tl, tr;
@@ -749,19 +762,6 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                     ref = hl ? cl : cr;
                     pop = false;
                 }
-            } else {
-                const int code = ~ref;
-                const int first = code >> 3, c = (code & 7) + 1;
-                TestRec cur = tests[first];
-                for (int k = first; k < first + c; k++) {
-                    const TestRec nxt = tests[k + 1]; // the record array carries one spare at the end
-                    if (STATS) {
-                        if ((__float_as_uint(cur.meta.y) & KIND_MASK) == RT_PRIM_TRIANGLE) cnt.tris++;
-                        else cnt.sphs++;
-                    }
-                    hit_any(cur, k, S.o, S.d, S.prev, xf, b);
-                    cur = nxt;
-                }
             }
             if (pop) {
                 if (sp > 0) {
@@ -770,6 +770,11 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                     trav = false;
                     done = true;
                 }
+            }
+            if (trav && ref < 0 && k >= kend) { // entering a leaf: its primitives come one per step
+                const int code = ~ref;
+                k = code >> 3;
+                kend = k + (code & 7) + 1;
             }
         }
         if (STATS) cnt.iters++;

@@ -14,4 +14,5 @@ rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/pmc2" -o pmc -- python3 
 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format csv -d "$out/pmc3" -o pmc -- python3 bench.py --no-cpu-baseline "$@" > "$out/pmc3.log" 2>&1
 rocprofv3 --pmc SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_INSTS_VALU_CVT --output-format csv -d "$out/pmc4" -o pmc -- python3 bench.py --no-cpu-baseline "$@" > "$out/pmc4.log" 2>&1
 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_WAIT_ANY SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_FLOPS_FP32 SQ_LDS_BANK_CONFLICT --output-format csv -d "$out/pmc5" -o pmc -- python3 bench.py --no-cpu-baseline "$@" > "$out/pmc5.log" 2>&1
+rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_DRAM_sum TCC_REQ_sum --output-format csv -d "$out/pmc6" -o pmc -- python3 bench.py --no-cpu-baseline "$@" > "$out/pmc6.log" 2>&1
 echo "profile $tag done"
