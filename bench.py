@@ -66,6 +66,28 @@ def bytes_per_ray(st, scene) -> float:
     return 32 + 16 + 32.0 * st["nodes"] + 48.0 * st["tris"] + st["sphs"] * (16.0 + 144.0 * xf_share) + 16.0 * n_pln + 48
 
 
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
+
+
+def roofline(cfg, fpr, bpr, rays, ms):
+    """C2/C3 (scene on chip) are bound by fp32 VALU issue; C4 (1M triangles, a
+    ~220 MB BVH + triangle set) by memory: its B_ray stream is priced against HBM."""
+    secs = ms * 1e-3
+    if cfg == "mesh1080":
+        gbs = bpr * rays / secs / 1e9
+        return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                "note": f"SURVEY B_ray {bpr:.0f} B per ray segment (node visits and triangle tests measured by the "
+                        f"instrumented kernel) x rays per launch / path-kernel time; compute view "
+                        f"{fpr * rays / secs / 1e12:.2f} TFLOP/s of {FP32_PEAK_TFLOPS}"}
+    tf = fpr * rays / secs / 1e12
+    return {"bound": "mfma", "achieved": round(tf, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": None,
+            "note": f"fp32 VALU kernel (no MFMA; the gfx950 fp32 vector and MFMA peaks are both 157.3 TFLOP/s); "
+                    f"{fpr:.0f} algorithmic FLOP per ray (SURVEY 8(d)); HBM view (SURVEY B_ray {bpr:.0f} B/ray, "
+                    f"scene served on chip): {bpr * rays / secs / 1e9:.0f} GB/s"}
+
+
 def path_stats(gpu, W, H, spp, seed, d_bufs):
     """One untimed instrumented launch: traversal work per ray segment and the wave-cycle split."""
     d_sum, d_n, d_m, d_rays = d_bufs
@@ -117,7 +139,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="bounce1080", choices=sorted(CONFIGS))
     ap.add_argument("--spp", type=int, default=0, help="override samples per pixel per step")
-    ap.add_argument("--traversal", default="auto", choices=["auto", "brute", "bvh"])
+    ap.add_argument("--traversal", default="auto", choices=["auto", "brute", "bvh", "bvh2"])
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -141,7 +163,8 @@ def main() -> int:
     if args.spp > 0:
         spp = args.spp
     scene = load_scene(rc, scene_file)
-    trav = {"auto": rc.RT_TRAVERSAL_AUTO, "brute": rc.RT_TRAVERSAL_BRUTE, "bvh": rc.RT_TRAVERSAL_BVH}[args.traversal]
+    trav = {"auto": rc.RT_TRAVERSAL_AUTO, "brute": rc.RT_TRAVERSAL_BRUTE, "bvh": rc.RT_TRAVERSAL_BVH,
+            "bvh2": rc.RT_TRAVERSAL_BVH2}[args.traversal]
     gpu = rc.GpuRaytracer(scene, cam, device=local, size=(W, H), traversal=trav)
     info = gpu.info()
     npix = W * H
@@ -209,7 +232,6 @@ def main() -> int:
         avg_ms = sum(kernel_ms) / len(kernel_ms)
         st = path_stats(gpu, W, H, max(1, spp // 16), args.seed, (d_sum, d_n, d_m, d_rays))
         fpr = flops_per_ray(st, scene)
-        achieved_tf = fpr * my_rays_per_step / (avg_ms * 1e-3) / 1e12
         bpr = bytes_per_ray(st, scene)
         out = {
             "metric": "Mrays/sec (primary+secondary) and samples/sec at 1080p, Cornell box",
@@ -225,17 +247,12 @@ def main() -> int:
             "dtype": "f32",
             "data": "synthetic: the reference's own scene file (tests/golden/scenes) with seeded camera samples",
             "config": {"workload": f"{scene_file} camera {cam} {W}x{H} x {spp} spp per GPU per step",
-                       "traversal": ["auto", "brute", "bvh"][info.traversal], "recursion": scene.params.recursion,
+                       "traversal": ["auto", "brute", "bvh4", "bvh2"][info.traversal], "recursion": scene.params.recursion,
                        "parallelism": f"sample-sharded x{world}, RCCL reduce per step"},
             "samples_per_s": round(total_samples / elapsed, 1),
             "rays_per_sample": round(total_rays / total_samples, 4),
             "kernel_ms": round(avg_ms, 3),
-            "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4), "traffic": None,
-                         "note": f"fp32 VALU kernel (no MFMA; the gfx950 fp32 vector and MFMA peaks are both "
-                                 f"157.3 TFLOP/s); {fpr:.0f} algorithmic FLOP per ray (SURVEY 8(d)); HBM view "
-                                 f"(SURVEY B_ray {bpr:.0f} B/ray, scene served on chip): "
-                                 f"{bpr * my_rays_per_step / (avg_ms * 1e-3) / 1e9:.0f} GB/s"},
+            "roofline": roofline(args.config, fpr, bpr, my_rays_per_step, avg_ms),
             "path_stats": {"per_ray": {k: round(st[k], 3) for k in ("nodes", "tris", "sphs")},
                            "lane_slots_per_ray": st["wave_iters_per_ray"]},
         }

@@ -124,9 +124,10 @@ typedef struct rt_scene rt_scene; /* opaque */
 
 /* Traversal strategy of the path-tracing kernel. */
 typedef enum rt_traversal {
-    RT_TRAVERSAL_AUTO = 0,  /* brute force for small scenes, BVH otherwise          */
-    RT_TRAVERSAL_BRUTE = 1, /* every primitive, scene read through the scalar cache */
-    RT_TRAVERSAL_BVH = 2    /* binned-SAH BVH2, per-lane LDS stack                  */
+    RT_TRAVERSAL_AUTO = 0,  /* brute force for small scenes, BVH otherwise            */
+    RT_TRAVERSAL_BRUTE = 1, /* every primitive, scene read through the scalar cache   */
+    RT_TRAVERSAL_BVH = 2,   /* 4-wide quantised BVH (binned SAH, collapsed), LDS stack */
+    RT_TRAVERSAL_BVH2 = 3   /* the binary binned-SAH BVH it is collapsed from          */
 } rt_traversal;
 
 typedef struct rt_scene_info {
@@ -207,10 +208,10 @@ int rt_last_kernel_ms(rt_scene* scene, float* ms);
  * path kernel's instrumented variant runs and adds up, over all launches since the last read,
  *   [0] BVH node visits  [1] triangle tests  [2] sphere tests           (per ray segment)
  *   [3] wave cycles in work fetch + camera ray  [4] in traversal  [5] in shading
- *   [6] wave loop iterations
+ *   [6] wave loop iterations  [7] BVH kernels: the most traversal steps one query took (max)
  * rt_scene_get_stats synchronises the device, copies min(n, RT_STATS_COUNT) counters and zeroes them.
  */
-#define RT_STATS_COUNT 7
+#define RT_STATS_COUNT 8
 int rt_scene_set_stats(rt_scene* scene, int32_t enable);
 int rt_scene_get_stats(rt_scene* scene, uint64_t* out, int32_t n);
 

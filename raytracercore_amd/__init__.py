@@ -26,7 +26,7 @@ RT_OK = 0
 RT_PRIM_TRIANGLE, RT_PRIM_SPHERE, RT_PRIM_PLANE = 0, 1, 2
 RT_FLAG_MIRROR, RT_FLAG_TWOSIDED, RT_FLAG_INVERT, RT_FLAG_HASNORMALS, RT_FLAG_TRANSFORMED = 1, 2, 4, 8, 16
 RT_CAMERA_FRUSTUM, RT_CAMERA_ORTHO = 0, 1
-RT_TRAVERSAL_AUTO, RT_TRAVERSAL_BRUTE, RT_TRAVERSAL_BVH = 0, 1, 2
+RT_TRAVERSAL_AUTO, RT_TRAVERSAL_BRUTE, RT_TRAVERSAL_BVH, RT_TRAVERSAL_BVH2 = 0, 1, 2, 3
 
 
 class RtError(RuntimeError):
@@ -281,7 +281,8 @@ class GpuRaytracer:
         _check(self.lib.rt_last_kernel_ms(self.handle, C.byref(ms)))
         return float(ms.value)
 
-    STAT_NAMES = ("node_visits", "tri_tests", "sph_tests", "cyc_start", "cyc_trace", "cyc_shade", "wave_iters")
+    STAT_NAMES = ("node_visits", "tri_tests", "sph_tests", "cyc_start", "cyc_trace", "cyc_shade", "wave_iters",
+                  "max_query_steps")
 
     def set_stats(self, enable: bool) -> None:
         """rt_scene_set_stats: run the instrumented kernel variant (profiling only)."""

@@ -231,4 +231,139 @@ SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf)
     return out;
 }
 
+// ---- 4-wide quantised BVH (Node4Q) -------------------------------------------------
+// Collapse the BVH2: each wide node opens the largest-area internal child until it holds four
+// children.  Child boxes are stored as 8-bit offsets from the node's origin in steps of 2^e
+// per axis, rounded outward (every child box is contained in its dequantised box, checked in
+// fp32), so a wide-node visit is one 64-B record as in the BVH2 and the depth halves.
+namespace {
+
+struct WChild {
+    FBox box;
+    int ref; // BVH2 child reference (>= 0 internal NodeF index, < 0 leaf code)
+};
+
+FBox nodef_box(const NodeF& n, bool right)
+{
+    FBox b;
+    const float4 lo = right ? n.rmin : n.lmin, hi = right ? n.rmax : n.lmax;
+    b.lo[0] = lo.x;
+    b.lo[1] = lo.y;
+    b.lo[2] = lo.z;
+    b.hi[0] = hi.x;
+    b.hi[1] = hi.y;
+    b.hi[2] = hi.z;
+    return b;
+}
+int nodef_ref(const NodeF& n, bool right)
+{
+    int r;
+    std::memcpy(&r, right ? &n.rmin.w : &n.lmin.w, 4);
+    return r;
+}
+
+struct W4Builder {
+    const std::vector<NodeF>& n2;
+    std::vector<Node4Q> out;
+    int stack_need = 0;
+    int depth = 0;
+
+    // Emit the wide node for BVH2 node i (pre-order); returns its index.
+    int emit(int i, int level, int pushes)
+    {
+        depth = std::max(depth, level);
+        std::vector<WChild> ch{{nodef_box(n2[i], false), nodef_ref(n2[i], false)},
+                               {nodef_box(n2[i], true), nodef_ref(n2[i], true)}};
+        while (ch.size() < 4) {
+            int best = -1;
+            float ba = -1.0f;
+            for (int k = 0; k < (int)ch.size(); k++)
+                if (ch[k].ref >= 0 && ch[k].box.area() > ba) {
+                    ba = ch[k].box.area();
+                    best = k;
+                }
+            if (best < 0) break;
+            const NodeF& m = n2[ch[best].ref];
+            WChild a{nodef_box(m, false), nodef_ref(m, false)}, b{nodef_box(m, true), nodef_ref(m, true)};
+            ch[best] = a;
+            ch.insert(ch.begin() + best + 1, b);
+        }
+        const int me = (int)out.size();
+        out.push_back(Node4Q{});
+        const int nc = (int)ch.size();
+        stack_need = std::max(stack_need, pushes + nc - 1);
+        int refs[4] = {RT_NODE4_EMPTY, RT_NODE4_EMPTY, RT_NODE4_EMPTY, RT_NODE4_EMPTY};
+        for (int k = 0; k < nc; k++)
+            refs[k] = ch[k].ref >= 0 ? emit(ch[k].ref, level + 1, pushes + nc - 1) : ch[k].ref;
+        // quantisation frame
+        FBox nb;
+        nb.empty();
+        for (const WChild& c : ch) nb.grow(c.box);
+        float org[3];
+        int ex[3];
+        uint32_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
+        for (int a = 0; a < 3; a++) {
+            org[a] = nb.lo[a];
+            const double ext = (double)nb.hi[a] - (double)nb.lo[a];
+            int e = ext > 0 ? (int)std::ceil(std::log2(ext / 255.0)) : -100;
+            e = std::max(e, -100);
+            while ((double)(float)((double)org[a] + 255.0 * std::ldexp(1.0, e)) < (double)nb.hi[a]) e++;
+            ex[a] = e;
+            const double sc = std::ldexp(1.0, e);
+            for (int k = 0; k < 4; k++) {
+                uint32_t lo8 = 255, hi8 = 0; // empty slot: inverted box
+                if (k < nc) {
+                    double ql = std::floor(((double)ch[k].box.lo[a] - (double)org[a]) / sc);
+                    double qh = std::ceil(((double)ch[k].box.hi[a] - (double)org[a]) / sc);
+                    ql = std::min(255.0, std::max(0.0, ql));
+                    qh = std::min(255.0, std::max(0.0, qh));
+                    // the fp32 dequantised planes must contain the child box
+                    while (ql > 0 && (float)((double)org[a] + ql * sc) > ch[k].box.lo[a]) ql -= 1;
+                    while (qh < 255 && (float)((double)org[a] + qh * sc) < ch[k].box.hi[a]) qh += 1;
+                    lo8 = (uint32_t)ql;
+                    hi8 = (uint32_t)qh;
+                }
+                qlo[a] |= lo8 << (8 * k);
+                qhi[a] |= hi8 << (8 * k);
+            }
+        }
+        Node4Q q;
+        uint32_t exps = (uint32_t)(ex[0] + 128) | ((uint32_t)(ex[1] + 128) << 8) | ((uint32_t)(ex[2] + 128) << 16);
+        auto f = [](uint32_t u) {
+            float v;
+            std::memcpy(&v, &u, 4);
+            return v;
+        };
+        auto fi = [](int u) {
+            float v;
+            std::memcpy(&v, &u, 4);
+            return v;
+        };
+        q.a = make_float4(org[0], org[1], org[2], f(exps));
+        q.b = make_float4(f(qlo[0]), f(qhi[0]), f(qlo[1]), f(qhi[1]));
+        q.c = make_float4(f(qlo[2]), f(qhi[2]), fi(refs[0]), fi(refs[1]));
+        q.d = make_float4(fi(refs[2]), fi(refs[3]), fi(nc), 0.0f);
+        out[me] = q;
+        return me;
+    }
+};
+
+} // namespace
+
+Bvh4 build_bvh4(const SahBvh& b2)
+{
+    Bvh4 r;
+    if (b2.nodes.empty()) { // a single leaf (or nothing)
+        r.root = b2.root;
+        return r;
+    }
+    W4Builder w{b2.nodes, {}, 0, 0};
+    w.out.reserve(b2.nodes.size() / 2 + 1);
+    r.root = w.emit(0, 0, 0);
+    r.nodes = std::move(w.out);
+    r.stack_need = w.stack_need;
+    r.depth = w.depth;
+    return r;
+}
+
 } // namespace rtc

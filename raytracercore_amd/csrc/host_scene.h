@@ -55,6 +55,14 @@ struct SahBvh {
 };
 SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf);
 
+struct Bvh4 {
+    std::vector<Node4Q> nodes;
+    int root = 0;       // child reference of the root (wide-node index or leaf code)
+    int stack_need = 0; // deepest traversal stack any ray can need
+    int depth = 0;
+};
+Bvh4 build_bvh4(const SahBvh& bvh2);
+
 // Camera.InitRender restated for both precisions.
 void camera_init(const rt_camera& cam, int width, int height, CameraD& d, CameraF& f);
 

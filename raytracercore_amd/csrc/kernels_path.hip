@@ -210,6 +210,15 @@ __device__ __forceinline__ void hit_any(const TestRec& R, int slot, V3 o, V3 d, 
     }
 }
 
+// 1/d for the box tests, with |d| clamped to >= 2^-64 so that an axis-parallel ray (d = 0 on an
+// axis, e.g. a diffuse bounce whose angle draw is exactly 0) gives large finite slab distances of
+// the right sign instead of 0 * inf = NaN, which the min/max chains would ignore (a box the ray
+// runs parallel to and outside of would then count as hit, and the query would visit every node).
+__device__ __forceinline__ float slab_rcp(float d)
+{
+    return rcp(fabsf(d) >= 5.421010862e-20f ? d : __builtin_copysignf(5.421010862e-20f, d));
+}
+
 __device__ __forceinline__ bool slab(float4 lo, float4 hi, V3 oi, V3 id, float tmax, float& tnear)
 {
     // t = box * (1/d) - o * (1/d); NaN from 0*inf is ignored by fminf/fmaxf (conservative)
@@ -222,8 +231,71 @@ __device__ __forceinline__ bool slab(float4 lo, float4 hi, V3 oi, V3 id, float t
     return tmin <= tmx * 1.00000024f;
 }
 
+// One visit of a 4-wide quantised node (Node4Q): slab tests of the four children against
+// dequantised planes t = q * (2^e / d) + (origin - o) / d, nearest hit child next, the other hit
+// children pushed far-to-near.  pop stays true when no child is hit.
+__device__ __forceinline__ float ubyte(uint32_t v, int k) { return (float)((v >> (8 * k)) & 255u); }
+__device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb)
+{
+    const bool sw = db < da;
+    const float t = da;
+    const int r = ra;
+    da = sw ? db : da;
+    ra = sw ? rb : ra;
+    db = sw ? t : db;
+    rb = sw ? r : rb;
+}
+template <int STACK>
+__device__ __forceinline__ void wide_visit(const Node4Q& q, V3 id, V3 oi, float best, int& ref, int& sp, int* stk,
+                                           bool& pop)
+{
+    const uint32_t ex = __float_as_uint(q.a.w);
+    const float ax = __builtin_amdgcn_ldexpf(id.x, (int)(ex & 255u) - 128);
+    const float ay = __builtin_amdgcn_ldexpf(id.y, (int)((ex >> 8) & 255u) - 128);
+    const float az = __builtin_amdgcn_ldexpf(id.z, (int)((ex >> 16) & 255u) - 128);
+    const float bx = fmaf(q.a.x, id.x, -oi.x), by = fmaf(q.a.y, id.y, -oi.y), bz = fmaf(q.a.z, id.z, -oi.z);
+    const uint32_t lx = __float_as_uint(q.b.x), hx = __float_as_uint(q.b.y);
+    const uint32_t ly = __float_as_uint(q.b.z), hy = __float_as_uint(q.b.w);
+    const uint32_t lz = __float_as_uint(q.c.x), hz = __float_as_uint(q.c.y);
+    // near / far planes by the direction's sign
+    const uint32_t nx = id.x >= 0.0f ? lx : hx, fx = id.x >= 0.0f ? hx : lx;
+    const uint32_t ny = id.y >= 0.0f ? ly : hy, fy = id.y >= 0.0f ? hy : ly;
+    const uint32_t nz = id.z >= 0.0f ? lz : hz, fz = id.z >= 0.0f ? hz : lz;
+    const int nc = __float_as_int(q.d.z);
+    float d0, d1, d2, d3;
+    int r0 = __float_as_int(q.c.z), r1 = __float_as_int(q.c.w), r2 = __float_as_int(q.d.x), r3 = __float_as_int(q.d.y);
+    const float tmax_best = best * 1.00000024f;
+#define RT_WIDE_CHILD(K, D)                                                                                       \
+    {                                                                                                             \
+        const float tmin = fmaxf(fmaxf(fmaxf(fmaf(ubyte(nx, K), ax, bx), fmaf(ubyte(ny, K), ay, by)),              \
+                                       fmaf(ubyte(nz, K), az, bz)), 0.0f);                                         \
+        const float tmax = fminf(fminf(fmaf(ubyte(fx, K), ax, bx), fmaf(ubyte(fy, K), ay, by)),                   \
+                                 fmaf(ubyte(fz, K), az, bz));                                                      \
+        D = (K < nc && tmin <= fminf(tmax * 1.00000024f, tmax_best)) ? tmin : __builtin_huge_valf();             \
+    }
+    RT_WIDE_CHILD(0, d0)
+    RT_WIDE_CHILD(1, d1)
+    RT_WIDE_CHILD(2, d2)
+    RT_WIDE_CHILD(3, d3)
+#undef RT_WIDE_CHILD
+    cswap(d0, r0, d1, r1);
+    cswap(d2, r2, d3, r3);
+    cswap(d0, r0, d2, r2);
+    cswap(d1, r1, d3, r3);
+    cswap(d1, r1, d2, r2);
+    const float inf = __builtin_huge_valf();
+    if (d0 < inf) {
+        if (d3 < inf && sp < STACK) stk[(sp++) * 256] = r3; // host guarantees the stack depth
+        if (d2 < inf && sp < STACK) stk[(sp++) * 256] = r2;
+        if (d1 < inf && sp < STACK) stk[(sp++) * 256] = r1;
+        ref = r0;
+        pop = false;
+    }
+}
+
 struct Counters {
     unsigned nodes, tris, sphs;                                  // per lane
+    unsigned q_steps, max_steps;                                 // per lane: steps of the current / longest query
     unsigned long long cyc_start, cyc_trace, cyc_shade, iters; // per wave (uniform)
 };
 
@@ -627,6 +699,9 @@ __device__ __forceinline__ void flush_counts(const Lane& L, const Counters& cnt,
             atomicAdd(p.stats + 5, cnt.cyc_shade);
             atomicAdd(p.stats + 6, cnt.iters);
         }
+        unsigned long long mx = cnt.max_steps;
+        for (int off = 32; off > 0; off >>= 1) mx = max(mx, (unsigned long long)__shfl_down(mx, off));
+        if (lane == 0) atomicMax(p.stats + 7, mx);
     }
 }
 
@@ -636,7 +711,8 @@ template <bool LDS, bool STATS>
 __global__ void __launch_bounds__(256, RT_PATH_WAVES)
     path_kernel(PathScene s, CameraF cam, PathParams p, const TestRec* __restrict__ tests,
                 const RectRec* __restrict__ rects, const PrimF* __restrict__ prims_g, const NodeF* __restrict__ nodes,
-                const XformF* __restrict__ xf, const MatF* __restrict__ mats_g, const float4* __restrict__ vnormals)
+                const Node4Q* __restrict__ nodes4, const XformF* __restrict__ xf, const MatF* __restrict__ mats_g,
+                const float4* __restrict__ vnormals)
 {
     extern __shared__ float4 lds_scene[];
     const ShadeRecs R = stage_scene<LDS>(s, prims_g, mats_g, xf, lds_scene);
@@ -685,12 +761,12 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
 // the shading / new-sample phase runs only once at least p.refill lanes wait (or none is still
 // traversing).  So one long traversal no longer holds the other 63 lanes of its wave, and the
 // divergent shading code is paid once per batch of finished queries.
-template <int STACK, bool LDS, bool STATS>
+template <int WIDTH, int STACK, bool LDS, bool STATS>
 __global__ void __launch_bounds__(256, RT_BVH_WAVES)
     path_kernel_bvh(PathScene s, CameraF cam, PathParams p, const TestRec* __restrict__ tests,
                     const RectRec* __restrict__ rects, const PrimF* __restrict__ prims_g,
-                    const NodeF* __restrict__ nodes, const XformF* __restrict__ xf, const MatF* __restrict__ mats_g,
-                    const float4* __restrict__ vnormals)
+                    const NodeF* __restrict__ nodes, const Node4Q* __restrict__ nodes4, const XformF* __restrict__ xf,
+                    const MatF* __restrict__ mats_g, const float4* __restrict__ vnormals)
 {
     __shared__ int stack_mem[STACK * 256];
     extern __shared__ float4 lds_scene[];
@@ -723,7 +799,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
             }
             refill(L, S, p, s, cam, lane, total);
             if (L.live && !trav) { // start the next query
-                id = v3(rcp(S.d.x), rcp(S.d.y), rcp(S.d.z));
+                id = v3(slab_rcp(S.d.x), slab_rcp(S.d.y), slab_rcp(S.d.z));
                 oi = S.o * id;
                 ref = s.root;
                 sp = 0;
@@ -746,6 +822,9 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                 }
                 hit_any(rec, k, S.o, S.d, S.prev, xf, b);
                 pop = ++k >= kend;
+            } else if (WIDTH == 4) {
+                wide_visit<STACK>(nodes4[ref], id, oi, b.t, ref, sp, stk, pop);
+                if (STATS) cnt.nodes++;
             } else {
                 const NodeF n = nodes[ref];
                 if (STATS) cnt.nodes++;
@@ -777,7 +856,14 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                 kend = k + (code & 7) + 1;
             }
         }
-        if (STATS) cnt.iters++;
+        if (STATS) {
+            cnt.iters++;
+            if (trav) cnt.q_steps++;
+            if (done) {
+                cnt.max_steps = max(cnt.max_steps, cnt.q_steps);
+                cnt.q_steps = 0;
+            }
+        }
     }
     flush_counts<STATS>(L, cnt, p, lane);
 }
@@ -822,28 +908,34 @@ __global__ void colors_1spp_kernel(PathParams p, double* out)
 }
 
 using PathKernel = void (*)(PathScene, CameraF, PathParams, const TestRec*, const RectRec*, const PrimF*,
-                            const NodeF*, const XformF*, const MatF*, const float4*);
+                            const NodeF*, const Node4Q*, const XformF*, const MatF*, const float4*);
 
 template <bool LDS>
 PathKernel pick_brute(bool stats)
 {
     return stats ? path_kernel<LDS, true> : path_kernel<LDS, false>;
 }
-template <int STACK, bool LDS>
+template <int WIDTH, int STACK, bool LDS>
 PathKernel pick_bvh(bool stats)
 {
-    return stats ? path_kernel_bvh<STACK, LDS, true> : path_kernel_bvh<STACK, LDS, false>;
+    return stats ? path_kernel_bvh<WIDTH, STACK, LDS, true> : path_kernel_bvh<WIDTH, STACK, LDS, false>;
 }
 
-// variant = traversal * 2 + lds; traversal 0 brute force, 1 BVH (24-entry stack), 2 BVH (48)
+// variant = kernel * 2 + lds; kernel 0 brute force, 1/2 BVH2 (24/48-entry stack), 3/4/5 wide BVH (32/40/64)
 PathKernel pick(int variant, bool stats)
 {
     switch (variant) {
     case 1: return pick_brute<true>(stats);
-    case 2: return pick_bvh<24, false>(stats);
-    case 3: return pick_bvh<24, true>(stats);
-    case 4: return pick_bvh<48, false>(stats);
-    case 5: return pick_bvh<48, true>(stats);
+    case 2: return pick_bvh<2, 24, false>(stats);
+    case 3: return pick_bvh<2, 24, true>(stats);
+    case 4: return pick_bvh<2, 48, false>(stats);
+    case 5: return pick_bvh<2, 48, true>(stats);
+    case 6: return pick_bvh<4, 32, false>(stats);
+    case 7: return pick_bvh<4, 32, true>(stats);
+    case 8: return pick_bvh<4, 40, false>(stats);
+    case 9: return pick_bvh<4, 40, true>(stats);
+    case 10: return pick_bvh<4, 64, false>(stats);
+    case 11: return pick_bvh<4, 64, true>(stats);
     default: return pick_brute<false>(stats);
     }
 }
@@ -879,11 +971,7 @@ size_t path_lds_bytes(const DevScene& s)
     return slots * sizeof(PrimF) + (size_t)s.n_ids * sizeof(MatF) + (size_t)s.n_xf * sizeof(XformF);
 }
 
-int path_variant(int traversal, int bvh_depth, bool lds)
-{
-    const int t = traversal != RT_TRAVERSAL_BVH ? 0 : (bvh_depth < 24 ? 1 : 2);
-    return t * 2 + (lds ? 1 : 0);
-}
+int path_variant(int kernel, bool lds) { return kernel * 2 + (lds ? 1 : 0); }
 
 int path_blocks_per_cu(int variant, size_t dyn_lds, bool stats)
 {
@@ -899,6 +987,7 @@ hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& 
                        hipStream_t stream, bool stats)
 {
     PathScene ps = make_path_scene(s);
+    if (variant >= 6) ps.root = s.root4; // the wide kernels walk the collapsed tree
     CameraF ca = cam;
     PathParams pa = p;
     const bool bvh = variant >= 2;
@@ -906,10 +995,11 @@ hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& 
     const RectRec* rects = s.rects_bf;
     const PrimF* prims = bvh ? s.prims_bvh : s.prims_bf;
     const NodeF* nodes = s.nodes;
+    const Node4Q* nodes4 = s.nodes4;
     const XformF* xf = s.xf;
     const MatF* mats = s.mats;
     const float4* vn = s.vnormals;
-    void* args[] = {&ps, &ca, &pa, &tests, &rects, &prims, &nodes, &xf, &mats, &vn};
+    void* args[] = {&ps, &ca, &pa, &tests, &rects, &prims, &nodes, &nodes4, &xf, &mats, &vn};
     const size_t dyn = (variant & 1) ? path_lds_bytes(s) : 0;
     return hipLaunchKernel(reinterpret_cast<const void*>(pick(variant, stats)), dim3(grid_blocks), dim3(256), args, dyn,
                            stream);

@@ -130,6 +130,17 @@ struct alignas(16) NodeF {      // 64 B: both children's boxes
     float4 rmax;
 };
 
+// 4-wide BVH node with 8-bit quantised child boxes (64 B, one visit = one record):
+//   a = (origin.xyz, exponents: (e_x + 128) | (e_y + 128) << 8 | (e_z + 128) << 16)
+//   b = (qlo_x, qhi_x, qlo_y, qhi_y), c = (qlo_z, qhi_z, child0, child1), d = (child2, child3, n_children, 0)
+// q* hold one byte per child (child k in bits 8k..8k+7): plane = origin + q * 2^e, rounded outward.
+// Child references as in NodeF (>= 0 wide-node index, < 0 leaf code); unused slots are
+// RT_NODE4_EMPTY with an inverted box.
+#define RT_NODE4_EMPTY ((int32_t)0x80000000)
+struct alignas(16) Node4Q {
+    float4 a, b, c, d;
+};
+
 struct CameraF {                // post-InitRender state in fp32 (path kernel)
     float4 position, look, side, up;
     float w2, h2, tan_x, tan_y, h_mult, v_mult, image_plane, dof, focal_length;
@@ -157,6 +168,9 @@ struct DevScene {
     const NodeF* nodes;
     int32_t n_nodes;
     int32_t root;               // child reference of the root (may be a leaf)
+    const Node4Q* nodes4;       // the same tree collapsed to 4-wide quantised nodes
+    int32_t n_nodes4;
+    int32_t root4;
     const XformF* xf;
     const MatF* mats;
     const float4* vnormals;     // 3 per primitive ID (HasNormals triangles)

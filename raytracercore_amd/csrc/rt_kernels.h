@@ -29,8 +29,9 @@ struct PathParams {
 hipError_t launch_primary_ids(const DevScene& s, const CameraD& cam, int x0, int y0, int w, int h, int32_t* d_ids,
                               hipStream_t stream);
 
-// Kernel variant for a traversal mode and BVH depth (the LDS stack must exceed the depth).
-int path_variant(int traversal, int bvh_depth, bool lds);
+// Kernel variant: kernel 0 brute force, 1/2 BVH2 (24/48-entry stack), 3/4/5 wide BVH (32/40/64);
+// lds stages the shading records in LDS.
+int path_variant(int kernel, bool lds);
 size_t path_lds_bytes(const DevScene& s);   // dynamic LDS of the staged (lds) variants
 // Launch the persistent kernel; stats counts node visits / primitive tests (slower build).
 hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& p, int variant, int grid_blocks,

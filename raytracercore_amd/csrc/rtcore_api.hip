@@ -90,11 +90,13 @@ struct rt_scene {
     int blocks_per_cu = 1;
     RefBvh ref;
     SahBvh sah;
+    Bvh4 bvh4;
     DevScene dev{};
     DevBuf<PrimF> prims_bf, prims_bvh;
     DevBuf<TestRec> tests_bf, tests_bvh;
     DevBuf<RectRec> rects_bf;
     DevBuf<NodeF> nodes;
+    DevBuf<Node4Q> nodes4;
     DevBuf<XformF> xf;
     DevBuf<MatF> mats;
     DevBuf<float4> vnormals;
@@ -325,11 +327,13 @@ int upload_scene(rt_scene* s)
     rects.push_back(RectRec{}); // one spare record: the kernel prefetches one past each group
     HIP_TRY(s->rects_bf.upload(rects));
     HIP_TRY(s->nodes.upload(s->sah.nodes));
+    HIP_TRY(s->nodes4.upload(s->bvh4.nodes));
     HIP_TRY(s->xf.upload(xf));
     HIP_TRY(s->mats.upload(mats));
     HIP_TRY(s->vnormals.upload(vn));
     s->device_bytes = pd.size() * sizeof(PrimD) + xd.size() * sizeof(XformD) + s->ref.nodes.size() * sizeof(RefNode) +
                       bf.size() * sizeof(PrimF) + bv.size() * sizeof(PrimF) + s->sah.nodes.size() * sizeof(NodeF) +
+                      s->bvh4.nodes.size() * sizeof(Node4Q) +
                       xf.size() * sizeof(XformF) + mats.size() * sizeof(MatF) + vn.size() * sizeof(float4);
 
     DevScene& d = s->dev;
@@ -345,6 +349,9 @@ int upload_scene(rt_scene* s)
     d.nodes = s->nodes.p;
     d.n_nodes = (int)s->sah.nodes.size();
     d.root = s->sah.root;
+    d.nodes4 = s->nodes4.p;
+    d.n_nodes4 = (int)s->bvh4.nodes.size();
+    d.root4 = s->bvh4.root;
     d.xf = s->xf.p;
     d.mats = s->mats.p;
     d.vnormals = s->vnormals.p;
@@ -372,15 +379,26 @@ int resolve_traversal(rt_scene* s)
         const int n_bvh = s->dev.n_rect[0] + s->dev.n_rect[1] + s->dev.n_rect[2] + s->dev.n_tri + s->dev.n_sph;
         t = n_bvh <= 48 ? RT_TRAVERSAL_BRUTE : RT_TRAVERSAL_BVH;
     }
-    if (t == RT_TRAVERSAL_BVH && s->sah.depth >= 48) {
-        set_error("BVH deeper than the kernel's LDS stack");
-        return RT_ERR_ARG;
+    // kernel: 0 brute force, 1/2 BVH2 with a 24/48-entry stack, 3/4/5 wide BVH with 32/40/64
+    int kernel = 0;
+    if (t == RT_TRAVERSAL_BVH2) {
+        if (s->sah.depth >= 48) {
+            set_error("BVH2 deeper than the kernel's LDS stack");
+            return RT_ERR_ARG;
+        }
+        kernel = s->sah.depth < 24 ? 1 : 2;
+    } else if (t == RT_TRAVERSAL_BVH) {
+        if (s->bvh4.stack_need > 64) {
+            set_error("wide BVH needs a deeper traversal stack than the kernel's 64 entries");
+            return RT_ERR_ARG;
+        }
+        kernel = s->bvh4.stack_need <= 32 ? 3 : s->bvh4.stack_need <= 40 ? 4 : 5;
     }
     s->resolved = t;
     // Stage the shading records in LDS when that costs no occupancy (RTCORE_PATH_LDS=0/1 forces
     // the choice for A/B measurements).
     const size_t lds = path_lds_bytes(s->dev);
-    const int plain = path_variant(t, s->sah.depth, false), staged = path_variant(t, s->sah.depth, true);
+    const int plain = path_variant(kernel, false), staged = path_variant(kernel, true);
     const int occ_plain = path_blocks_per_cu(plain, 0, false);
     const int occ_staged = lds <= 64 * 1024 ? path_blocks_per_cu(staged, lds, false) : 0;
     bool use_lds = occ_staged >= occ_plain;
@@ -518,6 +536,7 @@ int rt_scene_create(const rt_scene_params* params, const rt_prim* prims, int32_t
     s->host = prepare_prims(prims, n_prims);
     s->ref = build_ref_bvh(s->host);
     s->sah = build_sah_bvh(s->host, n_prims > 256 ? 4 : 2);
+    s->bvh4 = build_bvh4(s->sah);
     int rc = upload_scene(s.get());
     if (rc != RT_OK) return rc;
     rc = resolve_traversal(s.get());
@@ -540,7 +559,7 @@ int rt_scene_set_camera(rt_scene* s, const rt_camera* cam)
 
 int rt_scene_set_traversal(rt_scene* s, int32_t traversal)
 {
-    if (!s || traversal < RT_TRAVERSAL_AUTO || traversal > RT_TRAVERSAL_BVH) {
+    if (!s || traversal < RT_TRAVERSAL_AUTO || traversal > RT_TRAVERSAL_BVH2) {
         set_error("rt_scene_set_traversal: bad argument");
         return RT_ERR_ARG;
     }

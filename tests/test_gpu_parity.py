@@ -131,12 +131,13 @@ def test_sample_ranges_compose(rc, scenes):
     assert np.allclose(s1 + s2, s, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("mode", ["BVH", "BVH2"])
 @pytest.mark.parametrize("name", ["die.txt", "bounce.txt"])
-def test_traversal_modes_agree(rc, scenes, name):
-    """Brute force and BVH traversal return the same closest hits (same samples)."""
+def test_traversal_modes_agree(rc, scenes, name, mode):
+    """Brute force and BVH traversal (wide and binary) return the same closest hits."""
     scene = scenes[name]
     a = rc.GpuRaytracer(scene, 0, size=(128, 96), traversal=rc.RT_TRAVERSAL_BRUTE)
-    b = rc.GpuRaytracer(scene, 0, size=(128, 96), traversal=rc.RT_TRAVERSAL_BVH)
+    b = rc.GpuRaytracer(scene, 0, size=(128, 96), traversal=getattr(rc, "RT_TRAVERSAL_" + mode))
     sa, na, ma, ra = a.render_tile(0, 0, 128, 96, 16, seed=9)
     sb, nb, mb, rb = b.render_tile(0, 0, 128, 96, 16, seed=9)
     assert np.array_equal(na, nb) and np.array_equal(ma, mb)
@@ -144,15 +145,16 @@ def test_traversal_modes_agree(rc, scenes, name):
     assert np.allclose(sa, sb, rtol=1e-4, atol=1e-4)
 
 
-def test_traversal_modes_agree_mesh(rc):
+@pytest.mark.parametrize("mode", ["BVH", "BVH2"])
+def test_traversal_modes_agree_mesh(rc, mode):
     """The same on a small procedural height field (3,200 triangles): BVH == brute force up to
     ties on shared triangle edges."""
     from raytracercore_amd.scenes import mesh_scene_text
 
     scene = rc.SceneLoader.from_text(mesh_scene_text(nx=41, ny=41))
     a = rc.GpuRaytracer(scene, 0, size=(96, 64), traversal=rc.RT_TRAVERSAL_BRUTE)
-    b = rc.GpuRaytracer(scene, 0, size=(96, 64), traversal=rc.RT_TRAVERSAL_BVH)
-    assert b.info().traversal == rc.RT_TRAVERSAL_BVH
+    b = rc.GpuRaytracer(scene, 0, size=(96, 64), traversal=getattr(rc, "RT_TRAVERSAL_" + mode))
+    assert b.info().traversal == getattr(rc, "RT_TRAVERSAL_" + mode)
     sa, na, ma, ra = a.render_tile(0, 0, 96, 64, 16, seed=4)
     sb, nb, mb, rb = b.render_tile(0, 0, 96, 64, 16, seed=4)
     assert abs(int(ma.sum()) - int(mb.sum())) <= 2
