@@ -7,14 +7,17 @@
  * DEFINES the stream both the GPU kernels and the CPU oracle consume, so that a
  * sample of pixel (x, y) with index s makes the same decisions on both sides.
  *
- * Stream definition (normative):
- *   key   = splitmix64( splitmix64( splitmix64(seed) + pixel ) + sample )
- *           pixel  = y * frame_width + x   (whole-frame index, independent of tiling)
- *           sample = sample_base + s       (the s-th sample rendered for this pixel)
+ * Stream definition (normative; all arithmetic mod 2^32, H = lowbias32 below):
+ *   seed key   s0 = H(lo32(seed) + 0x9E3779B9),   s1 = H(hi32(seed) ^ 0x85EBCA6B ^ s0)
+ *   pixel key  p0 = H(lo32(pixel) ^ s0),           p1 = H(hi32(pixel) + p0 + s1)
+ *              pixel  = y * frame_width + x   (whole-frame index, independent of tiling)
+ *   sample key k0 = H(lo32(sample) ^ p0),          k1 = H(hi32(sample) + k0 + p1)
+ *              sample = sample_base + s       (the s-th sample rendered for this pixel)
  *   draw n (n = 0, 1, 2, ...):
- *           h = lowbias32( (lo32(key) + n * 0x9E3779B9) ^ hi32(key) )    (mod 2^32)
- *           U = (h >> 8) * 2^-24            in [0, 1 - 2^-24]
- *   i.e. one hash round of a Weyl sequence whose offset and mask are the per-sample key.
+ *              h = H( (k0 + n * 0x9E3779B9) ^ k1 )
+ *              U = (h >> 8) * 2^-24            in [0, 1 - 2^-24]
+ *   i.e. one hash round of a Weyl sequence whose offset and mask are the per-sample key;
+ *   only 32-bit multiplies, and a kernel hoists the seed and pixel keys out of its sample loop.
  * U has 24 significant bits, so it is exact in float and in double: the fp32 kernel
  * and the fp64 oracle see bit-identical uniforms.  Draws are consumed in the
  * reference's order: camera subX, subY, [dof radius, angle],
@@ -37,14 +40,6 @@
 extern "C" {
 #endif
 
-RT_HD uint64_t rt_splitmix64(uint64_t x)
-{
-    x += 0x9E3779B97F4A7C15ull;
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-    return x ^ (x >> 31);
-}
-
 RT_HD uint32_t rt_lowbias32(uint32_t x)
 {
     x ^= x >> 16;
@@ -56,31 +51,41 @@ RT_HD uint32_t rt_lowbias32(uint32_t x)
 }
 
 typedef struct rt_rng {
-    uint32_t k0; /* lo32(key) + n * 0x9E3779B9 for the next draw n */
-    uint32_t k1; /* hi32(key) */
+    uint32_t k0; /* sample key k0 + n * 0x9E3779B9 for the next draw n */
+    uint32_t k1; /* sample key k1 */
 } rt_rng;
 
-/* The key factors as seed_key = splitmix64(seed), pixel_key = splitmix64(seed_key + pixel),
- * key = splitmix64(pixel_key + sample): a kernel hoists the first two out of its sample loop. */
-RT_HD uint64_t rt_rng_pixel_key(uint64_t seed_key, uint64_t pixel) { return rt_splitmix64(seed_key + pixel); }
+typedef struct rt_key2 {
+    uint32_t a, b;
+} rt_key2;
 
-RT_HD rt_rng rt_rng_from_pixel_key(uint64_t pixel_key, uint64_t sample)
+RT_HD rt_key2 rt_rng_seed_key(uint64_t seed)
 {
-    uint64_t k = rt_splitmix64(pixel_key + sample);
-    rt_rng r;
-    r.k0 = (uint32_t)k;
-    r.k1 = (uint32_t)(k >> 32);
-    return r;
+    rt_key2 k;
+    k.a = rt_lowbias32((uint32_t)seed + 0x9E3779B9u);
+    k.b = rt_lowbias32((uint32_t)(seed >> 32) ^ 0x85EBCA6Bu ^ k.a);
+    return k;
 }
 
-RT_HD uint64_t rt_rng_key(uint64_t seed, uint64_t pixel, uint64_t sample)
+RT_HD rt_key2 rt_rng_pixel_key(rt_key2 seed_key, uint64_t pixel)
 {
-    return rt_splitmix64(rt_rng_pixel_key(rt_splitmix64(seed), pixel) + sample);
+    rt_key2 k;
+    k.a = rt_lowbias32((uint32_t)pixel ^ seed_key.a);
+    k.b = rt_lowbias32((uint32_t)(pixel >> 32) + k.a + seed_key.b);
+    return k;
+}
+
+RT_HD rt_rng rt_rng_from_pixel_key(rt_key2 pixel_key, uint64_t sample)
+{
+    rt_rng r;
+    r.k0 = rt_lowbias32((uint32_t)sample ^ pixel_key.a);
+    r.k1 = rt_lowbias32((uint32_t)(sample >> 32) + r.k0 + pixel_key.b);
+    return r;
 }
 
 RT_HD rt_rng rt_rng_init(uint64_t seed, uint64_t pixel, uint64_t sample)
 {
-    return rt_rng_from_pixel_key(rt_rng_pixel_key(rt_splitmix64(seed), pixel), sample);
+    return rt_rng_from_pixel_key(rt_rng_pixel_key(rt_rng_seed_key(seed), pixel), sample);
 }
 
 /* 24-bit draw as an integer in [0, 2^24). */

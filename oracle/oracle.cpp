@@ -566,6 +566,13 @@ int32_t orc_sample_output(rt_color sum, uint32_t samples, uint32_t misses, rt_co
     return code(std::pow(r, gamma), std::pow(g, gamma), std::pow(b, gamma), a);
 }
 
+int32_t orc_rng_draws(uint64_t seed, uint64_t pixel, uint64_t sample, int32_t n, double* out)
+{
+    rt_rng r = rt_rng_init(seed, pixel, sample);
+    for (int32_t k = 0; k < n; k++) out[k] = rt_rng_next_double(&r);
+    return 0;
+}
+
 double orc_fresnel(double cs, double ior_in, double ior_out)
 {
     double ratio_ = ior_in / ior_out;

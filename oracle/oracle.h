@@ -82,6 +82,9 @@ int32_t orc_sample_output(rt_color sum, uint32_t samples, uint32_t misses, rt_co
  * (returns 1 on total internal reflection). */
 double orc_fresnel(double cos_in, double ior_in, double ior_out);
 
+/* The shared random stream (include/rtcore_rng.h): the first n uniforms of (seed, pixel, sample). */
+int32_t orc_rng_draws(uint64_t seed, uint64_t pixel, uint64_t sample, int32_t n, double* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -60,6 +60,7 @@ def lib() -> C.CDLL:
                                               P(C.c_uint32), P(C.c_uint64), P(C.c_double), P(C.c_int32)]),
             "orc_sample_output": (C.c_int32, [rt_color, C.c_uint32, C.c_uint32, rt_color, C.c_double, C.c_double]),
             "orc_fresnel": (C.c_double, [C.c_double, C.c_double, C.c_double]),
+            "orc_rng_draws": (C.c_int32, [C.c_uint64, C.c_uint64, C.c_uint64, C.c_int32, C.POINTER(C.c_double)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -198,6 +199,13 @@ class OracleScene:
 
 def fresnel(cos_in: float, ior_in: float, ior_out: float) -> float:
     return lib().orc_fresnel(cos_in, ior_in, ior_out)
+
+
+def rng_draws(seed: int, pixel: int, sample: int, n: int) -> np.ndarray:
+    """The first n uniforms of the shared stream (include/rtcore_rng.h) for (seed, pixel, sample)."""
+    out = np.zeros(n, np.float64)
+    lib().orc_rng_draws(seed, pixel, sample, n, out.ctypes.data_as(C.POINTER(C.c_double)))
+    return out
 
 
 def sample_output(sum_rgb, samples, misses, background=(0, 0, 0), background_alpha=0.0, exposure=1.0) -> int:

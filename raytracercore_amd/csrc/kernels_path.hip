@@ -581,7 +581,7 @@ struct Lane {
     bool active, item_open, live;
     unsigned item;
     int fx, fy, s_next, s_end;
-    unsigned long long pkey; // rt_rng_pixel_key of the open item's pixel
+    rt_key2 pkey; // rt_rng_pixel_key of the open item's pixel
     float ar, ag, ab;
     unsigned n_s, n_m, rays;
     unsigned pool_next, pool_end;
@@ -593,7 +593,7 @@ __device__ __forceinline__ void lane_init(Lane& L)
     L.item_open = L.live = false;
     L.item = 0;
     L.fx = L.fy = L.s_next = L.s_end = 0;
-    L.pkey = 0;
+    L.pkey = rt_key2{0u, 0u};
     L.ar = L.ag = L.ab = 0.0f;
     L.n_s = L.n_m = L.rays = 0;
     L.pool_next = L.pool_end = 0;
@@ -623,13 +623,15 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const PathParams& p, 
             if (L.item >= total) {
                 L.active = false;
             } else {
-                unsigned c, q, by, bx;
-                divmod(L.item, (unsigned)p.n_pad, p.inv_n_pad, c, q);
-                divmod(q >> 6, (unsigned)p.blocks_x, p.inv_blocks_x, by, bx);
-                const int px = (int)bx * 8 + (q & 7), py = (int)by * 8 + ((q >> 3) & 7);
-                if (px < p.w && py < p.h) {
+                // item = ((block << log2_chunks) + chunk) * 64 + pixel of the 8x8 block
+                const unsigned q = L.item & 63u, t = L.item >> 6;
+                const int c = (int)(t & (unsigned)(p.n_chunks - 1));
+                unsigned by, bx;
+                divmod(t >> p.log2_chunks, (unsigned)p.blocks_x, p.inv_blocks_x, by, bx);
+                const int px = (int)bx * 8 + (q & 7), py = (int)by * 8 + (q >> 3);
+                if (px < p.w && py < p.h && c * p.chunk < p.spp) {
                     L.item_open = true;
-                    L.s_next = (int)c * p.chunk;
+                    L.s_next = c * p.chunk;
                     L.s_end = min(p.spp, L.s_next + p.chunk);
                     L.ar = L.ag = L.ab = 0.0f;
                     L.n_s = L.n_m = 0;
@@ -725,6 +727,7 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
     S.prev = -1;
     S.bounce = 0;
     Counters cnt{};
+    float exp_sink = 0.0f; // keeps the cost-experiment work alive (RT_EXP_*)
 
     while (true) {
         unsigned long long t0 = 0, t1 = 0, t2 = 0;
@@ -732,8 +735,23 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
         refill(L, S, p, s, cam, lane, total);
         if (!__any(L.active)) break;
         if (STATS) t1 = __builtin_readcyclecounter();
+#ifdef RT_EXP_DUP_START // cost experiment: a second camera sample on a copy
+        if (L.live) {
+            Sample S2 = S;
+            S2.rng.k0 ^= (unsigned)L.rays;
+            start_sample(cam, L.fx, L.fy, S2);
+            exp_sink += S2.o.x + S2.d.y;
+        }
+#endif
         if (L.live) {
             Best b{__builtin_huge_valf(), -1, 0.0f, 0.0f};
+#ifdef RT_EXP_DUP_TRACE // cost experiment: a second closest-hit query from a perturbed origin
+            {
+                Best b2{__builtin_huge_valf(), -1, 0.0f, 0.0f};
+                trace_brute(s, tests, rects, xf, S.o + v3(exp_sink * 1e-30f, 0, 0), S.d, S.prev, b2);
+                exp_sink += b2.t;
+            }
+#endif
             trace_brute(s, tests, rects, xf, S.o, S.d, S.prev, b);
             if (STATS) {
                 cnt.tris += s.n_rect[0] + s.n_rect[1] + s.n_rect[2] + s.n_tri;
@@ -741,6 +759,15 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
             }
             for (int i = pln0; i < pln0 + s.n_pln; i++) hit_plane(tests[i], i, S.o, S.d, S.prev, b);
             if (STATS) t2 = __builtin_readcyclecounter();
+#ifdef RT_EXP_DUP_SHADE // cost experiment: a second bounce on a copy
+            {
+                Sample S2 = S;
+                S2.rng.k0 ^= (unsigned)L.rays;
+                V3 c2;
+                shade(s, R.prims, R.mats, R.xfs, vnormals, b, S2, c2);
+                exp_sink += c2.x + S2.d.x;
+            }
+#endif
             bounce(L, S, s, R, vnormals, b);
         } else if (STATS) {
             t2 = __builtin_readcyclecounter();
@@ -753,6 +780,7 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
             cnt.iters++;
         }
     }
+    if (exp_sink == 1234.5f) p.partial[0].x = exp_sink;
     flush_counts<STATS>(L, cnt, p, lane);
 }
 
@@ -873,12 +901,14 @@ __global__ void accumulate_kernel(PathParams p, double* sum, uint32_t* samples, 
     const int x = blockIdx.x * 16 + (threadIdx.x & 15);
     const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
     if (x >= p.w || y >= p.h) return;
-    const int q = ((y >> 3) * p.blocks_x + (x >> 3)) * 64 + (y & 7) * 8 + (x & 7);
+    const size_t blk = (size_t)((y >> 3) * p.blocks_x + (x >> 3));
+    const int q = (y & 7) * 8 + (x & 7);
     const size_t npix = (size_t)p.w * p.h, i = (size_t)y * p.w + x;
     double r = sum[i], g = sum[npix + i], bl = sum[2 * npix + i];
     uint32_t ns = 0, nm = 0;
-    for (int c = 0; c < p.n_chunks; c++) {
-        const float4 v = p.partial[(size_t)c * p.n_pad + q];
+    const int used = (p.spp + p.chunk - 1) / p.chunk; // chunks past spp hold no partial
+    for (int c = 0; c < used; c++) {
+        const float4 v = p.partial[(((blk << p.log2_chunks) + c) << 6) + q];
         r += v.x;
         g += v.y;
         bl += v.z;
@@ -898,7 +928,7 @@ __global__ void colors_1spp_kernel(PathParams p, double* out)
     const int x = blockIdx.x * 16 + (threadIdx.x & 15);
     const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
     if (x >= p.w || y >= p.h) return;
-    const int q = ((y >> 3) * p.blocks_x + (x >> 3)) * 64 + (y & 7) * 8 + (x & 7);
+    const int q = ((y >> 3) * p.blocks_x + (x >> 3)) * 64 + (y & 7) * 8 + (x & 7); // 1 spp: one chunk
     const float4 v = p.partial[q];
     const bool miss = (__float_as_uint(v.w) & 0xFFFFu) == 0;
     const size_t o = ((size_t)x * p.h + y) * 3; // DoubleColor[w, h]: x*h + y

@@ -1,5 +1,6 @@
 // rt_kernels.h -- launch interface between the C ABI (rtcore_api.hip) and the kernels.
 #pragma once
+#include "../../include/rtcore_rng.h"
 #include "rt_internal.h"
 
 namespace rtc {
@@ -11,16 +12,17 @@ struct PathParams {
                                         // y0 + ((r / band) * band_stride + band_offset) * band + r % band
     int spp;                    // samples per pixel in this launch
     int chunk;                  // samples per work item (a lane owns one item at a time)
-    int n_chunks;               // ceil(spp / chunk)
+    int n_chunks;               // ceil(spp / chunk) rounded up to a power of two (empty chunks are skipped)
+    int log2_chunks;
     int blocks_x;               // 8x8 pixel blocks per tile row
     int n_pad;                  // padded pixels per chunk (blocks * 64)
     int refill;                 // BVH kernel: waiting lanes (of 64) that trigger the shading phase
-    float inv_n_pad, inv_blocks_x; // fp32 reciprocals for the item decode
+    float inv_blocks_x;         // fp32 reciprocal for the item decode
     unsigned long long seed;
-    unsigned long long seed_key;   // rt_splitmix64(seed) (rtcore_rng.h)
+    rt_key2 seed_key;           // rt_rng_seed_key(seed) (rtcore_rng.h)
     unsigned long long sample_base;
     unsigned int* counter;      // work-item dispenser (zeroed before launch), handed out 64 at a time
-    float4* partial;            // [n_chunks][n_pad]: rgb sums, (samples | misses << 16)
+    float4* partial;            // [block][chunk][64 pixels]: rgb sums, (samples | misses << 16)
     unsigned long long* rays;   // Scene.RayTrace-equivalents (added to)
     unsigned long long* stats;  // optional [7]: node visits, triangle tests, sphere tests (per lane);
                                 //   wave cycles in sample start, traversal, shading; wave iterations

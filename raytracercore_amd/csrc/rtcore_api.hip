@@ -423,15 +423,17 @@ PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint6
     int chunks = 32;
     if (const char* e = getenv("RTCORE_PATH_CHUNKS")) chunks = std::max(1, atoi(e));
     p.chunk = std::max(1, std::min(64, (spp + chunks - 1) / chunks));
-    p.n_chunks = (spp + p.chunk - 1) / p.chunk;
+    const int used = (spp + p.chunk - 1) / p.chunk;
+    p.log2_chunks = 0;
+    while ((1 << p.log2_chunks) < used) p.log2_chunks++;
+    p.n_chunks = 1 << p.log2_chunks; // work items: ((block << log2_chunks) + chunk) * 64 + pixel
     p.blocks_x = (w + 7) / 8;
     p.n_pad = p.blocks_x * ((h + 7) / 8) * 64;
-    p.inv_n_pad = 1.0f / (float)p.n_pad;
+    p.inv_blocks_x = 1.0f / (float)p.blocks_x;
     p.refill = 16;
     if (const char* e = getenv("RTCORE_BVH_REFILL")) p.refill = std::max(1, std::min(64, atoi(e)));
-    p.inv_blocks_x = 1.0f / (float)p.blocks_x;
     p.seed = seed;
-    p.seed_key = rt_splitmix64(seed);
+    p.seed_key = rt_rng_seed_key(seed);
     p.sample_base = base;
     return p;
 }

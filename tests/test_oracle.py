@@ -123,3 +123,48 @@ def test_threaded_frame_matches_sequential():
     b = s.render_tile(0, 0, 40, 30, 3, seed=2)
     assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and a[3] == b[3]
     assert np.allclose(a[0], b[0], rtol=1e-12, atol=0)
+
+
+def _h32(x):
+    x &= 0xFFFFFFFF
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & 0xFFFFFFFF
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & 0xFFFFFFFF
+    x ^= x >> 16
+    return x
+
+
+def _spec_draws(seed, pixel, sample, n):
+    """include/rtcore_rng.h's stream definition, restated in Python."""
+    m = 0xFFFFFFFF
+    s0 = _h32((seed & m) + 0x9E3779B9)
+    s1 = _h32((seed >> 32) ^ 0x85EBCA6B ^ s0)
+    p0 = _h32((pixel & m) ^ s0)
+    p1 = _h32((pixel >> 32) + p0 + s1)
+    k0 = _h32((sample & m) ^ p0)
+    k1 = _h32((sample >> 32) + k0 + p1)
+    return [(_h32(((k0 + i * 0x9E3779B9) & m) ^ k1) >> 8) * 2.0 ** -24 for i in range(n)]
+
+
+@pytest.mark.parametrize("seed,pixel,sample", [(0, 0, 0), (1, 12345, 7), (2**40 + 3, 2**33 + 5, 2**35 + 11)])
+def test_rng_matches_its_definition(seed, pixel, sample):
+    from oracle.oracle import rng_draws
+
+    assert list(rng_draws(seed, pixel, sample, 12)) == _spec_draws(seed, pixel, sample, 12)
+
+
+def test_rng_statistics():
+    """Uniformity (chi-square over 64 bins) and no lag-1 / cross-sample correlation for the draws
+    a path consumes: 20 draws of 4,000 samples over 4 pixels."""
+    from oracle.oracle import rng_draws
+
+    d = np.array([rng_draws(9, px, s, 20) for px in range(4) for s in range(1000)])
+    u = d.ravel()
+    hist = np.histogram(u, bins=64, range=(0, 1))[0]
+    exp = u.size / 64
+    chi2 = ((hist - exp) ** 2 / exp).sum()
+    assert chi2 < 120, chi2  # 63 dof: p ~ 1e-5
+    for a, b in [(d[:, :-1].ravel(), d[:, 1:].ravel()), (d[:-1].ravel(), d[1:].ravel())]:
+        assert abs(np.corrcoef(a, b)[0, 1]) < 0.02
+    assert abs(u.mean() - 0.5) < 0.005
