@@ -154,8 +154,13 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("RTCORE_BENCH_SAME_DEVICE") == "1":  # rehearsal of the N-rank path on one GPU
+        local = 0
     if world > 1:
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if os.environ.get("RTCORE_BENCH_SAME_DEVICE") == "1":  # RCCL refuses two ranks on one GPU
+            dist.init_process_group(backend="gloo")
+        else:
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -168,13 +173,12 @@ def main() -> int:
     gpu = rc.GpuRaytracer(scene, cam, device=local, size=(W, H), traversal=trav)
     info = gpu.info()
     npix = W * H
-    # frame accumulators (SampleSet[w, h]: sum RGB fp64, samples, misses) and one step's share
+    # frame accumulators (SampleSet[w, h]: sum RGB fp64, samples, misses) and two sets of one
+    # step's share: step k renders into set k % 2 while set (k-1) % 2 is reduced onto rank 0
     f_sum = torch.zeros(3 * npix, dtype=torch.float64, device=dev)
     f_n = torch.zeros(npix, dtype=torch.int32, device=dev)
     f_m = torch.zeros(npix, dtype=torch.int32, device=dev)
-    d_sum = torch.zeros_like(f_sum)
-    d_n = torch.zeros_like(f_n)
-    d_m = torch.zeros_like(f_m)
+    sets = [(torch.zeros_like(f_sum), torch.zeros_like(f_n), torch.zeros_like(f_m)) for _ in range(2)]
     d_rays = torch.zeros(1, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
@@ -182,33 +186,49 @@ def main() -> int:
 
     def step(k: int) -> None:
         base = sample_base(k, rank, world, spp)
+        d_sum, d_n, d_m = sets[k % 2]
         d_sum.zero_()
         d_n.zero_()
         d_m.zero_()
         gpu.render_device(0, 0, W, H, spp, args.seed, base, d_sum.data_ptr(), d_n.data_ptr(), d_m.data_ptr(),
                           d_rays.data_ptr(), stream)
 
-    def merge() -> None:
-        merge_accumulators([d_sum, d_n, d_m], dist)  # one RCCL reduce per accumulator plane
+    def start_merge(k: int):
+        # one RCCL reduce per accumulator plane, asynchronous: the next step's render (enqueued
+        # after this call) overlaps it on the compute stream
+        return k, merge_accumulators(sets[k % 2], dist, async_op=True)
+
+    def finish_merge(pending) -> None:
+        k, works = pending
+        for w in works:
+            w.wait()  # the compute stream waits for the reduce, not the host
         if rank == 0:
+            d_sum, d_n, d_m = sets[k % 2]
             f_sum.add_(d_sum)
             f_n.add_(d_n)
             f_m.add_(d_m)
 
-    for k in range(args.warmup):
-        step(k)
-        merge()
+    def run(first: int, count: int) -> list:
+        kernel_ms = []
+        pending = None
+        for k in range(first, first + count):
+            step(k)
+            kernel_ms.append(gpu.last_kernel_ms())  # hipEvent pair around this step's path kernel
+            if pending is not None:
+                finish_merge(pending)
+            pending = start_merge(k)
+        if pending is not None:
+            finish_merge(pending)
+        return kernel_ms
+
+    run(0, args.warmup)
     torch.cuda.synchronize(dev)
     d_rays.zero_()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    kernel_ms = []
     t0 = time.perf_counter()
-    for k in range(args.warmup, args.warmup + args.steps):
-        step(k)
-        kernel_ms.append(gpu.last_kernel_ms())  # hipEvent pair around the path kernel
-        merge()
+    kernel_ms = run(args.warmup, args.steps)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -230,7 +250,7 @@ def main() -> int:
             raise SystemExit(f"sample bookkeeping mismatch: {np.unique(n_all + m_all)} != {expect}")
         my_rays_per_step = total_rays / (args.steps * world)
         avg_ms = sum(kernel_ms) / len(kernel_ms)
-        st = path_stats(gpu, W, H, max(1, spp // 16), args.seed, (d_sum, d_n, d_m, d_rays))
+        st = path_stats(gpu, W, H, max(1, spp // 16), args.seed, (*sets[0], d_rays))
         fpr = flops_per_ray(st, scene)
         bpr = bytes_per_ray(st, scene)
         out = {

@@ -29,9 +29,10 @@ def band_rows(height: int, world: int, rank: int, band: int = 16) -> List[int]:
     return rows
 
 
-def merge_accumulators(tensors: Sequence, dist=None, dst: int = 0) -> None:
-    """Sum each rank's step accumulators onto `dst` (one reduce per tensor; no-op for 1 rank)."""
+def merge_accumulators(tensors: Sequence, dist=None, dst: int = 0, async_op: bool = False) -> list:
+    """Sum each rank's step accumulators onto `dst` (one reduce per tensor; no-op for 1 rank).
+    With async_op the work handles are returned; wait() on them before reading the result."""
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
-        return
-    for t in tensors:
-        dist.reduce(t, dst=dst)
+        return []
+    works = [dist.reduce(t, dst=dst, async_op=async_op) for t in tensors]
+    return [w for w in works if w is not None]

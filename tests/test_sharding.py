@@ -27,7 +27,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, async_merge=False):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -44,7 +44,9 @@ def _worker(rank, world, port, out_path):
     for step in range(STEPS):
         s, n, m, _ = orc.render_tile(0, 0, W, H, SPP, seed=5, sample_base=sample_base(step, rank, world, SPP))
         ts, tn, tm = torch.from_numpy(s), torch.from_numpy(n.astype(np.int64)), torch.from_numpy(m.astype(np.int64))
-        merge_accumulators([ts, tn, tm], dist)
+        works = merge_accumulators([ts, tn, tm], dist, async_op=async_merge)
+        for w in works:
+            w.wait()
         if rank == 0:
             f_sum += ts
             f_n += tn
@@ -55,9 +57,11 @@ def _worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-def test_sample_sharded_reduce_equals_single_render(tmp_path):
+@pytest.mark.parametrize("async_merge", [False, True])
+def test_sample_sharded_reduce_equals_single_render(tmp_path, async_merge):
+    """bench.py's merge: reduce each step's accumulators onto rank 0 (async as in bench.py)."""
     out = str(tmp_path / "merged.npz")
-    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), out, async_merge), nprocs=2, join=True)
     got = np.load(out)
     from oracle.oracle import OracleScene
 
