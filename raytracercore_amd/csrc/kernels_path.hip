@@ -162,7 +162,25 @@ template <int AXIS>
 __device__ __forceinline__ void rect_group(const RectRec* __restrict__ r, int n, V3 o, V3 d, V3 id, V3 oi, int prev,
                                            Best& b)
 {
+#ifdef RT_EXP_RECT_UNROLL4
+    for (; n >= 4; n -= 4, r += 4) {
+        const RectRec r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
+        hit_rect<AXIS>(r0, r0.sg, o, d, id, oi, prev, b);
+        hit_rect<AXIS>(r1, r1.sg, o, d, id, oi, prev, b);
+        hit_rect<AXIS>(r2, r2.sg, o, d, id, oi, prev, b);
+        hit_rect<AXIS>(r3, r3.sg, o, d, id, oi, prev, b);
+    }
+#endif
+#ifndef RT_EXP_RECT_NO_UNROLL
+    for (; n >= 2; n -= 2, r += 2) {
+        const RectRec r0 = r[0], r1 = r[1];
+        hit_rect<AXIS>(r0, r0.sg, o, d, id, oi, prev, b);
+        hit_rect<AXIS>(r1, r1.sg, o, d, id, oi, prev, b);
+    }
+    if (n > 0) hit_rect<AXIS>(*r, r->sg, o, d, id, oi, prev, b);
+#else
     for (; n > 0; n--, r++) hit_rect<AXIS>(*r, r->sg, o, d, id, oi, prev, b);
+#endif
 }
 
 // Every primitive in slot order (x-rects | y-rects | z-rects | triangles | spheres); the
