@@ -183,6 +183,14 @@ int rt_render_tile_1spp(rt_scene* scene, int32_t x0, int32_t y0, int32_t w, int3
  */
 int rt_primary_ids(rt_scene* scene, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t* ids_out);
 
+/*
+ * DebugRaycaster BoundingVolumes mode (DebugRaycaster.cs:200-212): for the same integer-pixel
+ * primary rays, BVH<T>.GetIntersectionCount (BVH.cs:352-363) over the reference BVH in fp64 --
+ * the number of nodes whose own box the ray meets (Volume.Intersect(ray).far >= 0), descending
+ * only through those.  counts_out[x*h + y]; 0 where the root is missed.
+ */
+int rt_bvh_counts(rt_scene* scene, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t* counts_out);
+
 /* -------------------------------------------------- device-resident renders --- */
 /*
  * The same work as rt_render_tile on device buffers (framebuffer stays in HBM).

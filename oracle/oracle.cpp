@@ -418,6 +418,30 @@ int32_t orc_primary_ids(const orc_scene* s, int32_t x0, int32_t y0, int32_t w, i
     return 0;
 }
 
+// BVH<T>.GetIntersectionCount (BVH.cs:352-363): nodes whose own volume the ray meets.
+static int32_t bvh_count(const BNode* n, const Ray& r)
+{
+    double nr, fr;
+    aabb_intersect(n->vol, r, nr, fr);
+    if (!(fr >= 0)) return 0;
+    if (n->leaf) return 1;
+    return 1 + bvh_count(n->left, r) + bvh_count(n->right, r);
+}
+
+int32_t orc_bvh_counts(const orc_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t* counts)
+{
+    if (!s || !counts || w < 0 || h < 0 || s->sc.cameras.empty()) return -1;
+    const Scene& sc = s->sc;
+    const Camera& cam = sc.cameras[sc.current_camera];
+    for (int x = 0; x < w; x++)
+        for (int y = 0; y < h; y++) {
+            Ray r = cam.get_ray(x0 + x, y0 + y); // DebugRaycaster.cs:241
+            r = Ray{ray_point(r, cam.image_plane), r.d};
+            counts[x * h + y] = sc.root ? bvh_count(sc.root, r) : 0;
+        }
+    return 0;
+}
+
 int32_t orc_raytrace(const orc_scene* s, const double o[4], const double d[4], double* dist)
 {
     if (!s) return -2;

@@ -51,6 +51,8 @@ int32_t orc_bvh_boxes(const orc_scene* s, double* boxes);
 
 /* DebugRaycaster Primitives mode, ids[x*h + y] (-1 = miss). */
 int32_t orc_primary_ids(const orc_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t* ids);
+/* DebugRaycaster BoundingVolumes mode: BVH<T>.GetIntersectionCount per integer-pixel ray (x*h + y). */
+int32_t orc_bvh_counts(const orc_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t* counts);
 /* Closest hit of an arbitrary ray with no skip hit: returns prim ID or -1; dist may be NULL. */
 int32_t orc_raytrace(const orc_scene* s, const double o[4], const double d[4], double* dist);
 

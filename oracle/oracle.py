@@ -50,6 +50,7 @@ def lib() -> C.CDLL:
             "orc_bvh_leaf_order": (C.c_int32, [C.c_void_p, P(C.c_int32)]),
             "orc_bvh_boxes": (C.c_int32, [C.c_void_p, P(C.c_double)]),
             "orc_primary_ids": (C.c_int32, [C.c_void_p] + [C.c_int32] * 4 + [P(C.c_int32)]),
+            "orc_bvh_counts": (C.c_int32, [C.c_void_p] + [C.c_int32] * 4 + [P(C.c_int32)]),
             "orc_raytrace": (C.c_int32, [C.c_void_p, P(C.c_double), P(C.c_double), P(C.c_double)]),
             "orc_sample": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int32, C.c_uint64, C.c_uint64, P(rt_color),
                                        P(C.c_int32)]),
@@ -160,6 +161,15 @@ class OracleScene:
         ids = np.empty((w, h), np.int32)
         assert lib().orc_primary_ids(self.h, x0, y0, w, h, ids.ctypes.data_as(C.POINTER(C.c_int32))) == 0
         return ids
+
+    def bvh_counts(self, x0=0, y0=0, w=None, h=None) -> np.ndarray:
+        """DebugRaycaster BoundingVolumes mode: BVH.GetIntersectionCount per pixel, [x, y]."""
+        W, H = self.size()
+        w = W - x0 if w is None else w
+        h = H - y0 if h is None else h
+        out = np.empty((w, h), np.int32)
+        assert lib().orc_bvh_counts(self.h, x0, y0, w, h, out.ctypes.data_as(C.POINTER(C.c_int32))) == 0
+        return out
 
     def raytrace(self, o, d) -> Tuple[int, float]:
         oa = (C.c_double * 4)(*o)

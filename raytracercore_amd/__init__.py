@@ -111,6 +111,7 @@ def load_library(path: str = "") -> C.CDLL:
                                      P(rt_color), P(C.c_uint32), P(C.c_uint32), P(C.c_uint64)]),
         "rt_render_tile_1spp": (C.c_int, [C.c_void_p] + [C.c_int32] * 4 + [C.c_uint64, C.c_uint64, P(rt_color)]),
         "rt_primary_ids": (C.c_int, [C.c_void_p] + [C.c_int32] * 4 + [P(C.c_int32)]),
+        "rt_bvh_counts": (C.c_int, [C.c_void_p] + [C.c_int32] * 4 + [P(C.c_int32)]),
         "rt_render_device": (C.c_int, [C.c_void_p] + [C.c_int32] * 5 + [C.c_uint64, C.c_uint64] +
                              [C.c_void_p] * 4 + [C.c_void_p]),
         "rt_primary_ids_device": (C.c_int, [C.c_void_p] + [C.c_int32] * 4 + [C.c_void_p, C.c_void_p]),
@@ -249,6 +250,14 @@ class GpuRaytracer:
         ids = np.empty((w, h), np.int32)
         _check(self.lib.rt_primary_ids(self.handle, x0, y0, w, h, ids.ctypes.data_as(C.POINTER(C.c_int32))))
         return ids
+
+    def bvh_counts(self, x0: int = 0, y0: int = 0, w: Optional[int] = None, h: Optional[int] = None) -> np.ndarray:
+        """DebugRaycaster BoundingVolumes mode: reference-BVH node counts as int32 [x, y]."""
+        w = self.width - x0 if w is None else w
+        h = self.height - y0 if h is None else h
+        out = np.empty((w, h), np.int32)
+        _check(self.lib.rt_bvh_counts(self.handle, x0, y0, w, h, out.ctypes.data_as(C.POINTER(C.c_int32))))
+        return out
 
     def render_tile(self, x0: int, y0: int, w: int, h: int, spp: int, seed: int = 0, sample_base: int = 0):
         """Accumulators (sum[w,h,3] f64, samples[w,h] u32, misses[w,h] u32, rays)."""

@@ -131,37 +131,107 @@ __device__ static int cmp_near(double a, double b) // double.CompareTo
     return (a != a) ? ((b != b) ? 0 : -1) : 1;
 }
 
-// Returns the primitive ID, -1 on a miss, -2 if the pierced-leaf list overflowed.
-__device__ int ref_raytrace(const DevScene& s, Vec4d o, Vec4d d)
+struct LeafItem {
+    int node;
+    double nr, fr;
+};
+
+// The leaf scan of Scene.RayTracePrimitives (Scene.cs:74-91) over leaves given in sorted order.
+struct LeafScan {
+    int best = -1;
+    double best_d = 0, prev_far = 0;
+    bool have_prev = false;
+    // returns false once the `Near > previous.Far` break is reached
+    __device__ bool visit(const DevScene& s, const LeafItem& it, Vec4d o, Vec4d d)
+    {
+        if (have_prev && it.nr > prev_far) return false;
+        HitD h;
+        if (prim_raytrace_d(s, s.ref_nodes[it.node].prim, o, d, h) && (best < 0 || h.dist < best_d)) {
+            best = h.prim;
+            best_d = h.dist;
+            prev_far = it.fr;
+            have_prev = true;
+        }
+        return true;
+    }
+};
+
+// (near, DFS ordinal) in the order of the stable insertion sort with double.CompareTo
+__device__ static bool key_less(double an, int ao, double bn, int bo)
 {
-    if (s.n_ref_nodes == 0) return -1;
-    struct Item {
-        int node;
-        double nr, fr;
-    };
-    Item leaves[kLeafCap];
-    int nl = 0;
-    Item stack[kStackCap];
-    int sp = 0;
-    stack[sp++] = Item{0, 0.0, 0.0};
+    const int c = cmp_near(an, bn);
+    return c < 0 || (c == 0 && ao < bo);
+}
+
+// BVH<T>.IntersectLeaves (BVH.cs:295-331) as an explicit depth-first walk: calls f(item, ordinal)
+// for every pierced leaf in the order the reference appends them.
+template <class F>
+__device__ static bool walk_leaves(const DevScene& s, Vec4d o, Vec4d d, F&& f)
+{
+    LeafItem stack[kStackCap];
+    int sp = 0, ord = 0;
+    stack[sp++] = LeafItem{0, 0.0, 0.0};
     while (sp > 0) {
-        Item it = stack[--sp];
+        LeafItem it = stack[--sp];
         const RefNode& n = s.ref_nodes[it.node];
         if (!n.skip) {
             aabb_hit_ref(n.mn, n.mx, o, d, it.nr, it.fr);
             if (!(it.fr >= 0)) continue;
         }
         if (n.prim >= 0) {
-            if (nl == kLeafCap) return -2;
-            leaves[nl++] = it;
+            f(it, ord++);
             continue;
         }
-        if (sp + 2 > kStackCap) return -2;
-        stack[sp++] = Item{n.right, it.nr, it.fr};
-        stack[sp++] = Item{it.node + 1, it.nr, it.fr};
+        if (sp + 2 > kStackCap) return false;
+        stack[sp++] = LeafItem{n.right, it.nr, it.fr};
+        stack[sp++] = LeafItem{it.node + 1, it.nr, it.fr};
     }
+    return true;
+}
+
+// Same result when more than kLeafCap leaves are pierced (large meshes): the leaves are taken in
+// sorted order by repeated selection, one depth-first walk per leaf the scan consumes (the scan
+// usually stops after a few leaves), so no list is stored.
+__device__ static int ref_raytrace_select(const DevScene& s, Vec4d o, Vec4d d)
+{
+    LeafScan scan;
+    double cur_n = 0;
+    int cur_o = -1;
+    bool first = true;
+    while (true) {
+        LeafItem next{-1, 0.0, 0.0};
+        int next_o = -1;
+        const bool ok = walk_leaves(s, o, d, [&](const LeafItem& it, int ord) {
+            if (!first && !key_less(cur_n, cur_o, it.nr, ord)) return; // already consumed
+            if (next_o < 0 || key_less(it.nr, ord, next.nr, next_o)) {
+                next = it;
+                next_o = ord;
+            }
+        });
+        if (!ok) return -2;
+        if (next_o < 0 || !scan.visit(s, next, o, d)) break;
+        cur_n = next.nr;
+        cur_o = next_o;
+        first = false;
+    }
+    return scan.best;
+}
+
+// Returns the primitive ID, -1 on a miss, -2 if the traversal stack overflowed.
+__device__ int ref_raytrace(const DevScene& s, Vec4d o, Vec4d d)
+{
+    if (s.n_ref_nodes == 0) return -1;
+    LeafItem leaves[kLeafCap];
+    int nl = 0;
+    bool overflow = false;
+    const bool ok = walk_leaves(s, o, d, [&](const LeafItem& it, int) {
+        if (nl < kLeafCap) leaves[nl++] = it;
+        else overflow = true;
+    });
+    if (!ok) return -2;
+    if (overflow) return ref_raytrace_select(s, o, d);
     for (int i = 1; i < nl; i++) { // Util.InsertSort, stable
-        Item a = leaves[i];
+        LeafItem a = leaves[i];
         int j = i - 1;
         while (j >= 0 && cmp_near(a.nr, leaves[j].nr) < 0) {
             leaves[j + 1] = leaves[j];
@@ -169,20 +239,33 @@ __device__ int ref_raytrace(const DevScene& s, Vec4d o, Vec4d d)
         }
         leaves[j + 1] = a;
     }
-    int best = -1;
-    double best_d = 0, prev_far = 0;
-    bool have_prev = false;
-    for (int i = 0; i < nl; i++) {
-        if (have_prev && leaves[i].nr > prev_far) break;
-        HitD h;
-        if (prim_raytrace_d(s, s.ref_nodes[leaves[i].node].prim, o, d, h) && (best < 0 || h.dist < best_d)) {
-            best = h.prim;
-            best_d = h.dist;
-            prev_far = leaves[i].fr;
-            have_prev = true;
-        }
+    LeafScan scan;
+    for (int i = 0; i < nl; i++)
+        if (!scan.visit(s, leaves[i], o, d)) break;
+    return scan.best;
+}
+
+// BVH<T>.GetIntersectionCount (BVH.cs:352-363), DebugRaycaster BoundingVolumes mode: the nodes
+// whose own box the ray meets (Volume.Intersect(ray).far >= 0), descending only through them.
+__device__ int ref_bvh_count(const DevScene& s, Vec4d o, Vec4d d)
+{
+    if (s.n_ref_nodes == 0) return 0;
+    int stack[kStackCap];
+    int sp = 0, count = 0;
+    stack[sp++] = 0;
+    while (sp > 0) {
+        const int i = stack[--sp];
+        const RefNode& n = s.ref_nodes[i];
+        double nr, fr;
+        aabb_hit_ref(n.mn, n.mx, o, d, nr, fr);
+        if (!(fr >= 0)) continue;
+        count++;
+        if (n.prim >= 0) continue;
+        if (sp + 2 > kStackCap) return -2;
+        stack[sp++] = n.right;
+        stack[sp++] = i + 1;
     }
-    return best;
+    return count;
 }
 
 __device__ static void camera_ray_d(const CameraD& c, double x, double y, Vec4d& o, Vec4d& d)
@@ -200,21 +283,23 @@ __device__ static void camera_ray_d(const CameraD& c, double x, double y, Vec4d&
     o = add(o, scale(d, c.image_plane)); // Ray.Offset (Ray.cs:59-62)
 }
 
-__global__ void __launch_bounds__(64) primary_ids_kernel(DevScene s, CameraD cam, int x0, int y0, int w, int h, int32_t* ids)
+// mode 0: primary hit IDs (Primitives mode), mode 1: BVH node counts (BoundingVolumes mode)
+__global__ void __launch_bounds__(64) primary_ids_kernel(DevScene s, CameraD cam, int x0, int y0, int w, int h, int mode,
+                                                         int32_t* ids)
 {
     int x = blockIdx.x * 8 + (threadIdx.x & 7);
     int y = blockIdx.y * 8 + (threadIdx.x >> 3);
     if (x >= w || y >= h) return;
     Vec4d o, d;
     camera_ray_d(cam, (double)(x0 + x), (double)(y0 + y), o, d);
-    ids[(size_t)y * w + x] = ref_raytrace(s, o, d);
+    ids[(size_t)y * w + x] = mode == 0 ? ref_raytrace(s, o, d) : ref_bvh_count(s, o, d);
 }
 
-hipError_t launch_primary_ids(const DevScene& s, const CameraD& cam, int x0, int y0, int w, int h, int32_t* d_ids,
-                              hipStream_t stream)
+hipError_t launch_primary_ids(const DevScene& s, const CameraD& cam, int x0, int y0, int w, int h, int mode,
+                              int32_t* d_ids, hipStream_t stream)
 {
     dim3 grid((w + 7) / 8, (h + 7) / 8);
-    hipLaunchKernelGGL(primary_ids_kernel, grid, dim3(64), 0, stream, s, cam, x0, y0, w, h, d_ids);
+    hipLaunchKernelGGL(primary_ids_kernel, grid, dim3(64), 0, stream, s, cam, x0, y0, w, h, mode, d_ids);
     return hipGetLastError();
 }
 

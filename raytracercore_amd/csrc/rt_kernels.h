@@ -28,8 +28,9 @@ struct PathParams {
                                 //   wave cycles in sample start, traversal, shading; wave iterations
 };
 
-hipError_t launch_primary_ids(const DevScene& s, const CameraD& cam, int x0, int y0, int w, int h, int32_t* d_ids,
-                              hipStream_t stream);
+// mode 0: primary hit IDs, mode 1: reference-BVH node counts (DebugRaycaster BoundingVolumes)
+hipError_t launch_primary_ids(const DevScene& s, const CameraD& cam, int x0, int y0, int w, int h, int mode,
+                              int32_t* d_ids, hipStream_t stream);
 
 // Kernel variant: kernel 0 brute force, 1/2 BVH2 (24/48-entry stack), 3/4/5 wide BVH (32/40/64);
 // lds stages the shading records in LDS.

@@ -727,31 +727,39 @@ int rt_render_tile_1spp(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t 
     return RT_OK;
 }
 
-int rt_primary_ids_device(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t* d_ids, void* stream)
+} // extern "C"
+
+namespace {
+
+// The exact fp64 debug passes (DebugRaycaster.cs:170-212): mode 0 primary hit IDs, mode 1
+// reference-BVH node counts.  Device output is row-major over the tile.
+int debug_pass_device(rt_scene* s, int mode, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t* d_out,
+                      hipStream_t stream, const char* name)
 {
     int rc = check_tile(s, x0, y0, w, h);
     if (rc != RT_OK) return rc;
-    if (!d_ids) {
-        set_error("rt_primary_ids_device: bad argument");
+    if (!d_out) {
+        set_error(std::string(name) + ": bad argument");
         return RT_ERR_ARG;
     }
     HIP_TRY(hipSetDevice(s->device));
-    HIP_TRY(launch_primary_ids(s->dev, s->camd, x0, y0, w, h, d_ids, static_cast<hipStream_t>(stream)));
+    HIP_TRY(launch_primary_ids(s->dev, s->camd, x0, y0, w, h, mode, d_out, stream));
     return RT_OK;
 }
 
-int rt_primary_ids(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t* ids_out)
+// The same into a host buffer in the DoubleColor[w, h]-style x*h + y order.
+int debug_pass_host(rt_scene* s, int mode, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t* out, const char* name)
 {
     int rc = check_tile(s, x0, y0, w, h);
     if (rc != RT_OK) return rc;
-    if (!ids_out) {
-        set_error("rt_primary_ids: bad argument");
+    if (!out) {
+        set_error(std::string(name) + ": bad argument");
         return RT_ERR_ARG;
     }
     HIP_TRY(hipSetDevice(s->device));
     const size_t npix = (size_t)w * h;
     HIP_TRY(s->ids.reserve(npix));
-    rc = rt_primary_ids_device(s, x0, y0, w, h, s->ids.p, s->stream);
+    rc = debug_pass_device(s, mode, x0, y0, w, h, s->ids.p, s->stream, name);
     if (rc != RT_OK) return rc;
     std::vector<int32_t> tmp(npix);
     HIP_TRY(hipMemcpyAsync(tmp.data(), s->ids.p, npix * sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
@@ -761,13 +769,32 @@ int rt_primary_ids(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, in
         for (int x = 0; x < w; x++) {
             int32_t v = tmp[(size_t)y * w + x];
             overflow |= v == -2;
-            ids_out[(size_t)x * h + y] = v;
+            out[(size_t)x * h + y] = v;
         }
     if (overflow) {
-        set_error("rt_primary_ids: a ray pierced more leaves than the exact kernel's list holds");
+        set_error(std::string(name) + ": the reference BVH is deeper than the exact kernel's traversal stack");
         return RT_ERR_STATE;
     }
     return RT_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int rt_primary_ids_device(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t* d_ids, void* stream)
+{
+    return debug_pass_device(s, 0, x0, y0, w, h, d_ids, static_cast<hipStream_t>(stream), "rt_primary_ids_device");
+}
+
+int rt_primary_ids(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t* ids_out)
+{
+    return debug_pass_host(s, 0, x0, y0, w, h, ids_out, "rt_primary_ids");
+}
+
+int rt_bvh_counts(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t* counts_out)
+{
+    return debug_pass_host(s, 1, x0, y0, w, h, counts_out, "rt_bvh_counts");
 }
 
 int rt_render_frame_multi(const rt_scene_params* params, const rt_prim* prims, int32_t n_prims,

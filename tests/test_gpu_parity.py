@@ -40,6 +40,34 @@ def test_primary_ids_bitexact_1080p(rc, scenes, name):
     assert (ids >= 0).any() and (ids == -1).any()
 
 
+@pytest.mark.parametrize("cam", [0, 2])
+@pytest.mark.parametrize("name", ["bounce.txt", "die.txt"])
+def test_bvh_counts_bitexact(rc, scenes, name, cam):
+    """DebugRaycaster BoundingVolumes mode: reference-BVH node counts, exact."""
+    scene = scenes[name]
+    gpu = rc.GpuRaytracer(scene, cam, size=(640, 360))
+    got = gpu.bvh_counts()
+    ref = _oracle(rc, scene, (640, 360), cam).bvh_counts()
+    assert np.array_equal(got, ref)
+    assert got.max() > 3 and (got == 0).any() == (ref == 0).any()
+
+
+def test_mesh_primary_ids_bitexact(rc):
+    """1M-triangle mesh (config C4): grazing rays pierce more leaves than the exact kernel's list
+    holds, so this also covers its selection fallback; IDs must still be exact."""
+    from raytracercore_amd.scenes import mesh_scene_text
+
+    scene = rc.SceneLoader.from_text(mesh_scene_text())
+    size = (120, 68)
+    gpu = rc.GpuRaytracer(scene, 0, size=size)
+    ids = gpu.primary_ids()
+    ref = _oracle(rc, scene, size).primary_ids()
+    assert int((ids != ref).sum()) == 0
+    assert (ids >= 11).mean() > 0.02  # the height field (IDs after the room and light box) is in view
+    counts = gpu.bvh_counts(40, 20, 24, 16)
+    assert np.array_equal(counts, _oracle(rc, scene, size).bvh_counts(40, 20, 24, 16))
+
+
 @pytest.mark.parametrize("name", ["bounce.txt", "die.txt"])
 def test_primary_ids_tile_offsets(rc, scenes, name):
     """A sub-tile equals the same window of the full frame (tile origin handling)."""
