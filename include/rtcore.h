@@ -253,6 +253,14 @@ int rt_parse_scene(const char* text, rt_scene_params* params, rt_prim* prims, in
 int rt_ref_bvh_export(const rt_prim* prims, int32_t n_prims, int32_t* leaf_order, double* boxes,
                       int32_t* n_nodes, int32_t* depth);
 
+/*
+ * SampleSet.GetOutput (SampleSet.cs:61-113) on the device, for every pixel of accumulators in
+ * rt_render_device's layout (row-major w*h, d_sum planes R | G | B): d_argb[y*w + x] receives the
+ * Color.ToArgb code the UI bitmap stores.  Uses the calling thread's current device.  Asynchronous.
+ */
+int rt_tonemap_device(const double* d_sum, const uint32_t* d_samples, const uint32_t* d_misses, int32_t w, int32_t h,
+                      rt_color background, double background_alpha, double exposure, int32_t* d_argb, void* stream);
+
 /* SampleSet.GetOutput (SampleSet.cs:61-113): tonemap accumulators to ARGB. */
 int32_t rt_sample_output(rt_color sum, uint32_t samples, uint32_t misses, rt_color background,
                          double background_alpha, double exposure);

@@ -124,6 +124,8 @@ def load_library(path: str = "") -> C.CDLL:
         "rt_parse_scene": (C.c_int, [C.c_char_p, P(rt_scene_params), P(rt_prim), P(C.c_int32), P(rt_camera),
                                      P(C.c_int32)]),
         "rt_sample_output": (C.c_int32, [rt_color, C.c_uint32, C.c_uint32, rt_color, C.c_double, C.c_double]),
+        "rt_tonemap_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, rt_color, C.c_double,
+                                        C.c_double, C.c_void_p, C.c_void_p]),
         "rt_ref_bvh_export": (C.c_int, [P(rt_prim), C.c_int32, P(C.c_int32), P(C.c_double), P(C.c_int32),
                                         P(C.c_int32)]),
     }
@@ -302,6 +304,14 @@ class GpuRaytracer:
         out = (C.c_uint64 * len(self.STAT_NAMES))()
         _check(self.lib.rt_scene_get_stats(self.handle, out, len(self.STAT_NAMES)))
         return dict(zip(self.STAT_NAMES, (int(v) for v in out)))
+
+
+def tonemap_device(d_sum: int, d_samples: int, d_misses: int, w: int, h: int, d_argb: int,
+                   background=(0.0, 0.0, 0.0), background_alpha: float = 0.0, exposure: float = 1.0,
+                   stream: int = 0) -> None:
+    """rt_tonemap_device: SampleSet.GetOutput for every pixel of device accumulators (pointers)."""
+    _check(load_library().rt_tonemap_device(d_sum, d_samples, d_misses, w, h, rt_color(*background),
+                                            background_alpha, exposure, d_argb, stream))
 
 
 def render_frame_multi(scene: ParsedScene, camera_index: int, n_gpus: int, spp: int, seed: int = 0,

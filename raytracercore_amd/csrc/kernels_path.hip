@@ -941,6 +941,41 @@ __global__ void accumulate_kernel(PathParams p, double* sum, uint32_t* samples, 
     misses[i] += nm;
 }
 
+// SampleSet.GetOutput / GetColorCode (SampleSet.cs:50-113) per pixel of planar accumulators.
+__device__ __forceinline__ uint32_t color_code(double r, double g, double b, double a)
+{
+    auto q = [](double v) { // Util.Clamp to [0, 1], then (int)(v * 255)
+        v = v > 0.0 ? v : 0.0;
+        v = v < 1.0 ? v : 1.0;
+        return (uint32_t)(int32_t)(v * 255);
+    };
+    return (q(a) << 24) | (q(r) << 16) | (q(g) << 8) | q(b);
+}
+
+__global__ void tonemap_kernel(int w, int h, const double* __restrict__ sum, const uint32_t* __restrict__ samples,
+                               const uint32_t* __restrict__ misses, double br, double bg, double bb, double back_alpha,
+                               double exposure, int32_t* __restrict__ argb)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n = w * h;
+    if (i >= n) return;
+    const uint32_t ns = samples[i], nm = misses[i];
+    if (ns == 0) {
+        argb[i] = (int32_t)color_code(br * exposure, bg * exposure, bb * exposure, back_alpha);
+        return;
+    }
+    const double total = (double)ns + (double)nm;
+    const double mult = exposure / ns;
+    double r = sum[i] * mult, g = sum[n + i] * mult, b = sum[2 * (size_t)n + i] * mult, a = 1;
+    const double bam = nm / total, bk = bam * back_alpha;
+    r += (br - r) * bk;
+    g += (bg - g) * bk;
+    b += (bb - b) * bk;
+    a += (back_alpha - a) * bam;
+    const double gamma = 1 / 2.2;
+    argb[i] = (int32_t)color_code(pow(r, gamma), pow(g, gamma), pow(b, gamma), a);
+}
+
 __global__ void colors_1spp_kernel(PathParams p, double* out)
 {
     const int x = blockIdx.x * 16 + (threadIdx.x & 15);
@@ -1057,6 +1092,15 @@ hipError_t launch_accumulate(const PathParams& p, double* d_sum, uint32_t* d_sam
 {
     dim3 grid((p.w + 15) / 16, (p.h + 15) / 16);
     hipLaunchKernelGGL(accumulate_kernel, grid, dim3(256), 0, stream, p, d_sum, d_samples, d_misses);
+    return hipGetLastError();
+}
+
+hipError_t launch_tonemap(int w, int h, const double* d_sum, const uint32_t* d_samples, const uint32_t* d_misses,
+                          rt_color back, double back_alpha, double exposure, int32_t* d_argb, hipStream_t stream)
+{
+    const int n = w * h;
+    hipLaunchKernelGGL(tonemap_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, w, h, d_sum, d_samples, d_misses,
+                       back.r, back.g, back.b, back_alpha, exposure, d_argb);
     return hipGetLastError();
 }
 

@@ -44,6 +44,9 @@ int path_blocks_per_cu(int variant, size_t dyn_lds, bool stats);
 // partial -> fp64 planar accumulators (d_sum[3][w*h], d_samples, d_misses), added to.
 hipError_t launch_accumulate(const PathParams& p, double* d_sum, uint32_t* d_samples, uint32_t* d_misses,
                              hipStream_t stream);
+// SampleSet.GetOutput over planar accumulators (row-major w*h) -> ARGB codes.
+hipError_t launch_tonemap(int w, int h, const double* d_sum, const uint32_t* d_samples, const uint32_t* d_misses,
+                          rt_color back, double back_alpha, double exposure, int32_t* d_argb, hipStream_t stream);
 // partial (1 spp) -> DoubleColor[w, h] in x*h + y order, Placeholder(-1) on a miss.
 hipError_t launch_colors_1spp(const PathParams& p, double* d_out, hipStream_t stream);
 

@@ -990,6 +990,18 @@ int rt_ref_bvh_export(const rt_prim* prims, int32_t n, int32_t* leaf_order, doub
     return RT_OK;
 }
 
+int rt_tonemap_device(const double* d_sum, const uint32_t* d_samples, const uint32_t* d_misses, int32_t w, int32_t h,
+                      rt_color background, double background_alpha, double exposure, int32_t* d_argb, void* stream)
+{
+    if (!d_sum || !d_samples || !d_misses || !d_argb || w <= 0 || h <= 0) {
+        set_error("rt_tonemap_device: bad argument");
+        return RT_ERR_ARG;
+    }
+    HIP_TRY(launch_tonemap(w, h, d_sum, d_samples, d_misses, background, background_alpha, exposure, d_argb,
+                           static_cast<hipStream_t>(stream)));
+    return RT_OK;
+}
+
 int32_t rt_sample_output(rt_color sum, uint32_t n_samples, uint32_t n_misses, rt_color back, double back_alpha,
                          double exposure)
 {

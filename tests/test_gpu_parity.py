@@ -208,3 +208,34 @@ def test_errors_fail_loudly(rc, scenes):
         gpu.render_tile(60, 60, 8, 8, 1)  # outside the frame
     with pytest.raises(rc.RtError):
         gpu.primary_ids(0, 0, 0, 4)
+
+
+def test_tonemap_device_matches_sample_output(rc, scenes):
+    """SampleSet.GetOutput on the device (rt_tonemap_device) against the oracle's per-pixel
+    restatement on the same accumulators: ARGB codes equal, up to a 1-LSB truncation flip where
+    device and host pow differ in the last ulp."""
+    import torch
+    from oracle.oracle import sample_output
+
+    W, H = 64, 48
+    gpu = rc.GpuRaytracer(scenes["die.txt"], 0, size=(W, H))
+    dev = torch.device("cuda", 0)
+    s = torch.zeros(3 * W * H, dtype=torch.float64, device=dev)
+    n = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    m = torch.zeros_like(n)
+    r = torch.zeros(1, dtype=torch.int64, device=dev)
+    gpu.render_device(0, 0, W, H, 8, 3, 0, s.data_ptr(), n.data_ptr(), m.data_ptr(), r.data_ptr(), 0)
+    out = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    back, alpha, expo = (0.2, 0.3, 0.4), 0.5, 1.7
+    rc.tonemap_device(s.data_ptr(), n.data_ptr(), m.data_ptr(), W, H, out.data_ptr(), back, alpha, expo)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    sh, nh, mh = s.cpu().numpy().reshape(3, -1), n.cpu().numpy(), m.cpu().numpy()
+    ref = np.array([sample_output(tuple(sh[:, i]), int(nh[i]), int(mh[i]), back, alpha, expo) & 0xFFFFFFFF
+                    for i in range(W * H)], dtype=np.uint32)
+    assert (mh > 0).any() and (nh > 0).any()
+    diff = got != ref
+    assert diff.mean() < 1e-3
+    for k in range(4):  # any difference is one code step in one channel
+        ch = lambda a: (a >> (8 * k)) & 255
+        assert np.abs(ch(got).astype(int) - ch(ref).astype(int)).max() <= 1
