@@ -565,6 +565,9 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
 #ifndef RT_PATH_WAVES
 #define RT_PATH_WAVES 6 // minimum waves per SIMD the register allocator must allow (brute force)
 #endif
+#ifndef RT_LEAF_STEP
+#define RT_LEAF_STEP 2 // leaf primitives tested per BVH traversal step
+#endif
 #ifndef RT_BVH_WAVES
 #define RT_BVH_WAVES 5 // the same for the BVH kernel (its LDS stack caps occupancy anyway)
 #endif
@@ -860,14 +863,27 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
         }
         if (trav) { // one traversal step: one node visit, or one primitive of the current leaf
             bool pop = true; // child references are node indices or ~leaf codes (any int)
-            if (k < kend) {
-                const TestRec rec = tests[k];
+            if (k < kend) { // up to RT_LEAF_STEP primitives, their loads issued together
+                const TestRec r0 = tests[k];
+#if RT_LEAF_STEP >= 2
+                const TestRec r1 = tests[k + 1]; // the record array carries a spare at the end
+#endif
                 if (STATS) {
-                    if ((__float_as_uint(rec.meta.y) & KIND_MASK) == RT_PRIM_TRIANGLE) cnt.tris++;
+                    if ((__float_as_uint(r0.meta.y) & KIND_MASK) == RT_PRIM_TRIANGLE) cnt.tris++;
                     else cnt.sphs++;
                 }
-                hit_any(rec, k, S.o, S.d, S.prev, xf, b);
-                pop = ++k >= kend;
+                hit_any(r0, k, S.o, S.d, S.prev, xf, b);
+#if RT_LEAF_STEP >= 2
+                if (k + 1 < kend) {
+                    if (STATS) {
+                        if ((__float_as_uint(r1.meta.y) & KIND_MASK) == RT_PRIM_TRIANGLE) cnt.tris++;
+                        else cnt.sphs++;
+                    }
+                    hit_any(r1, k + 1, S.o, S.d, S.prev, xf, b);
+                }
+#endif
+                k += RT_LEAF_STEP;
+                pop = k >= kend;
             } else if (WIDTH == 4) {
                 wide_visit<STACK>(nodes4[ref], id, oi, b.t, ref, sp, stk, pop);
                 if (STATS) cnt.nodes++;
