@@ -132,7 +132,8 @@ typedef enum rt_traversal {
 
 typedef struct rt_scene_info {
     int32_t n_prims;
-    int32_t ref_bvh_nodes;   /* nodes of the reference agglomerative BVH (BVH.cs:193-236) */
+    int32_t ref_bvh_nodes;   /* nodes of the reference agglomerative BVH (BVH.cs:193-236); 0 until
+                                the first exact debug pass builds it                         */
     int32_t ref_bvh_depth;
     int32_t sah_bvh_nodes;   /* nodes of the kernel's BVH2                                */
     int32_t sah_bvh_depth;

@@ -89,6 +89,7 @@ struct rt_scene {
     int variant = 0;
     int blocks_per_cu = 1;
     RefBvh ref;
+    bool ref_built = false;
     SahBvh sah;
     Bvh4 bvh4;
     DevScene dev{};
@@ -317,7 +318,6 @@ int upload_scene(rt_scene* s)
     }
     HIP_TRY(s->prims_d.upload(pd));
     HIP_TRY(s->xf_d.upload(xd));
-    HIP_TRY(s->ref_nodes.upload(s->ref.nodes));
     HIP_TRY(s->prims_bf.upload(bf));
     HIP_TRY(s->prims_bvh.upload(bv));
     tbf.push_back(TestRec{}); // spare records: the brute-force loops prefetch one ahead
@@ -331,7 +331,7 @@ int upload_scene(rt_scene* s)
     HIP_TRY(s->xf.upload(xf));
     HIP_TRY(s->mats.upload(mats));
     HIP_TRY(s->vnormals.upload(vn));
-    s->device_bytes = pd.size() * sizeof(PrimD) + xd.size() * sizeof(XformD) + s->ref.nodes.size() * sizeof(RefNode) +
+    s->device_bytes = pd.size() * sizeof(PrimD) + xd.size() * sizeof(XformD) +
                       bf.size() * sizeof(PrimF) + bv.size() * sizeof(PrimF) + s->sah.nodes.size() * sizeof(NodeF) +
                       s->bvh4.nodes.size() * sizeof(Node4Q) +
                       xf.size() * sizeof(XformF) + mats.size() * sizeof(MatF) + vn.size() * sizeof(float4);
@@ -359,8 +359,8 @@ int upload_scene(rt_scene* s)
     d.n_xf = (int)xf.size();
     d.prims_d = s->prims_d.p;
     d.xf_d = s->xf_d.p;
-    d.ref_nodes = s->ref_nodes.p;
-    d.n_ref_nodes = (int)s->ref.nodes.size();
+    d.ref_nodes = nullptr; // built on first use (ensure_ref_bvh)
+    d.n_ref_nodes = 0;
     d.width = s->params.width;
     d.height = s->params.height;
     d.recursion = s->params.recursion;
@@ -369,6 +369,21 @@ int upload_scene(rt_scene* s)
     const rt_color& a = s->params.ambient;
     d.ambient = make_float3((float)a.r, (float)a.g, (float)a.b);
     d.ambient_miss = (a.r == -1 && a.g == -1 && a.b == -1) ? 1 : 0; // AmbientRGB == Placeholder
+    return RT_OK;
+}
+
+// The reference agglomerative BVH (BVH.cs:12-236) serves only the exact debug passes; it is built
+// and uploaded on first use, so a render-only scene does not pay for it (5.8 s for 1 M triangles).
+int ensure_ref_bvh(rt_scene* s)
+{
+    if (s->ref_built) return RT_OK;
+    s->ref = build_ref_bvh(s->host);
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(s->ref_nodes.upload(s->ref.nodes));
+    s->dev.ref_nodes = s->ref_nodes.p;
+    s->dev.n_ref_nodes = (int)s->ref.nodes.size();
+    s->device_bytes += s->ref.nodes.size() * sizeof(RefNode);
+    s->ref_built = true;
     return RT_OK;
 }
 
@@ -536,7 +551,6 @@ int rt_scene_create(const rt_scene_params* params, const rt_prim* prims, int32_t
     HIP_TRY(hipEventCreate(&s->ev0));
     HIP_TRY(hipEventCreate(&s->ev1));
     s->host = prepare_prims(prims, n_prims);
-    s->ref = build_ref_bvh(s->host);
     s->sah = build_sah_bvh(s->host, n_prims > 256 ? 4 : 2);
     s->bvh4 = build_bvh4(s->sah);
     int rc = upload_scene(s.get());
@@ -742,6 +756,8 @@ int debug_pass_device(rt_scene* s, int mode, int32_t x0, int32_t y0, int32_t w, 
         set_error(std::string(name) + ": bad argument");
         return RT_ERR_ARG;
     }
+    rc = ensure_ref_bvh(s);
+    if (rc != RT_OK) return rc;
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(launch_primary_ids(s->dev, s->camd, x0, y0, w, h, mode, d_out, stream));
     return RT_OK;
