@@ -139,7 +139,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="bounce1080", choices=sorted(CONFIGS))
     ap.add_argument("--spp", type=int, default=0, help="override samples per pixel per step")
-    ap.add_argument("--traversal", default="auto", choices=["auto", "brute", "bvh", "bvh2"])
+    ap.add_argument("--traversal", default="auto", choices=["auto", "brute", "bvh", "bvh2", "grouped"])
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -169,7 +169,7 @@ def main() -> int:
         spp = args.spp
     scene = load_scene(rc, scene_file)
     trav = {"auto": rc.RT_TRAVERSAL_AUTO, "brute": rc.RT_TRAVERSAL_BRUTE, "bvh": rc.RT_TRAVERSAL_BVH,
-            "bvh2": rc.RT_TRAVERSAL_BVH2}[args.traversal]
+            "bvh2": rc.RT_TRAVERSAL_BVH2, "grouped": rc.RT_TRAVERSAL_GROUPED}[args.traversal]
     gpu = rc.GpuRaytracer(scene, cam, device=local, size=(W, H), traversal=trav)
     info = gpu.info()
     npix = W * H
@@ -267,7 +267,7 @@ def main() -> int:
             "dtype": "f32",
             "data": "synthetic: the reference's own scene file (tests/golden/scenes) with seeded camera samples",
             "config": {"workload": f"{scene_file} camera {cam} {W}x{H} x {spp} spp per GPU per step",
-                       "traversal": ["auto", "brute", "bvh4", "bvh2"][info.traversal], "recursion": scene.params.recursion,
+                       "traversal": ["auto", "brute", "bvh4", "bvh2", "grouped"][info.traversal], "recursion": scene.params.recursion,
                        "parallelism": f"sample-sharded x{world}, RCCL reduce per step"},
             "samples_per_s": round(total_samples / elapsed, 1),
             "rays_per_sample": round(total_rays / total_samples, 4),

@@ -124,10 +124,13 @@ typedef struct rt_scene rt_scene; /* opaque */
 
 /* Traversal strategy of the path-tracing kernel. */
 typedef enum rt_traversal {
-    RT_TRAVERSAL_AUTO = 0,  /* brute force for small scenes, BVH otherwise            */
+    RT_TRAVERSAL_AUTO = 0,  /* small scenes: brute force, grouped where a cost model
+                               favours it; large scenes: the wide BVH                  */
     RT_TRAVERSAL_BRUTE = 1, /* every primitive, scene read through the scalar cache   */
     RT_TRAVERSAL_BVH = 2,   /* 4-wide quantised BVH (binned SAH, collapsed), LDS stack */
-    RT_TRAVERSAL_BVH2 = 3   /* the binary binned-SAH BVH it is collapsed from          */
+    RT_TRAVERSAL_BVH2 = 3,  /* the binary binned-SAH BVH it is collapsed from          */
+    RT_TRAVERSAL_GROUPED = 4 /* brute force over groups of <= 8 primitives, a group
+                                skipped when no ray of the wave meets its box          */
 } rt_traversal;
 
 typedef struct rt_scene_info {

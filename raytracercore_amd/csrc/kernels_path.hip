@@ -183,51 +183,6 @@ __device__ __forceinline__ void rect_group(const RectRec* __restrict__ r, int n,
 #endif
 }
 
-// Every primitive in slot order (x-rects | y-rects | z-rects | triangles | spheres); the
-// loop index is wave-uniform, so the records arrive through scalar loads.
-__device__ __forceinline__ void trace_brute(const PathScene& s, const TestRec* __restrict__ tests,
-                                            const RectRec* __restrict__ rects, const XformF* __restrict__ xf, V3 o,
-                                            V3 d, int prev, Best& b)
-{
-    int i = 0;
-    if (s.n_rect[0] + s.n_rect[1] + s.n_rect[2] > 0) {
-        const V3 id = v3(rcp(d.x), rcp(d.y), rcp(d.z));
-        const V3 oi = o * id;
-        rect_group<0>(rects, s.n_rect[0], o, d, id, oi, prev, b);
-        rect_group<1>(rects + s.n_rect[0], s.n_rect[1], o, d, id, oi, prev, b);
-        rect_group<2>(rects + s.n_rect[0] + s.n_rect[1], s.n_rect[2], o, d, id, oi, prev, b);
-        i = s.n_rect[0] + s.n_rect[1] + s.n_rect[2];
-    }
-    int end = i + s.n_tri;
-    if (i < end) {
-        TestRec cur = tests[i];
-        for (; i < end; i++) {
-            const TestRec nxt = tests[i + 1];
-            hit_tri(cur, i, o, d, prev, b);
-            cur = nxt;
-        }
-    }
-    end = i + s.n_sph;
-    if (i < end) {
-        TestRec cur = tests[i];
-        for (; i < end; i++) {
-            const TestRec nxt = tests[i + 1];
-            hit_sph(cur, i, o, d, prev, xf, b);
-            cur = nxt;
-        }
-    }
-}
-
-__device__ __forceinline__ void hit_any(const TestRec& R, int slot, V3 o, V3 d, int prev, const XformF* __restrict__ xf,
-                                        Best& b)
-{
-    switch (__float_as_uint(R.meta.y) & KIND_MASK) {
-    case RT_PRIM_TRIANGLE: hit_tri(R, slot, o, d, prev, b); break;
-    case RT_PRIM_SPHERE: hit_sph(R, slot, o, d, prev, xf, b); break;
-    default: hit_plane(R, slot, o, d, prev, b); break;
-    }
-}
-
 // 1/d for the box tests, with |d| clamped to >= 2^-64 so that an axis-parallel ray (d = 0 on an
 // axis, e.g. a diffuse bounce whose angle draw is exactly 0) gives large finite slab distances of
 // the right sign instead of 0 * inf = NaN, which the min/max chains would ignore (a box the ray
@@ -248,6 +203,66 @@ __device__ __forceinline__ bool slab(float4 lo, float4 hi, V3 oi, V3 id, float t
     tnear = tmin;
     return tmin <= tmx * 1.00000024f;
 }
+
+// Every primitive, group by group (GroupRec: x-rects | y-rects | z-rects | triangles | spheres).
+// The loop indices are wave-uniform, so the records arrive through scalar loads.  With CULL a
+// group is skipped when no lane of the wave meets its box before its current closest hit.
+template <bool CULL, bool STATS>
+__device__ __forceinline__ void trace_brute(const PathScene& s, const GroupRec* __restrict__ groups,
+                                            const TestRec* __restrict__ tests, const RectRec* __restrict__ rects,
+                                            const XformF* __restrict__ xf, V3 o, V3 d, int prev, Best& b,
+                                            unsigned& n_flat, unsigned& n_sph)
+{
+    const V3 id = v3(slab_rcp(d.x), slab_rcp(d.y), slab_rcp(d.z));
+    const V3 oi = o * id;
+    for (int g = 0; g < s.n_groups; g++) {
+        const GroupRec G = groups[g];
+        if (CULL) {
+            float tn;
+            if (!__any(slab(G.lo, G.hi, oi, id, b.t, tn))) continue;
+        }
+        if (STATS) { // primitive tests actually made (groups the wave skipped are not counted)
+            n_flat += G.n_rect[0] + G.n_rect[1] + G.n_rect[2] + (G.n_tri_sph & 0xFFFF);
+            n_sph += G.n_tri_sph >> 16;
+        }
+        const RectRec* r = rects + __float_as_int(G.lo.w);
+        rect_group<0>(r, G.n_rect[0], o, d, id, oi, prev, b);
+        r += G.n_rect[0];
+        rect_group<1>(r, G.n_rect[1], o, d, id, oi, prev, b);
+        r += G.n_rect[1];
+        rect_group<2>(r, G.n_rect[2], o, d, id, oi, prev, b);
+        int i = __float_as_int(G.hi.w);
+        int end = i + (G.n_tri_sph & 0xFFFF);
+        if (i < end) {
+            TestRec cur = tests[i];
+            for (; i < end; i++) {
+                const TestRec nxt = tests[i + 1];
+                hit_tri(cur, i, o, d, prev, b);
+                cur = nxt;
+            }
+        }
+        end = i + (G.n_tri_sph >> 16);
+        if (i < end) {
+            TestRec cur = tests[i];
+            for (; i < end; i++) {
+                const TestRec nxt = tests[i + 1];
+                hit_sph(cur, i, o, d, prev, xf, b);
+                cur = nxt;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void hit_any(const TestRec& R, int slot, V3 o, V3 d, int prev, const XformF* __restrict__ xf,
+                                        Best& b)
+{
+    switch (__float_as_uint(R.meta.y) & KIND_MASK) {
+    case RT_PRIM_TRIANGLE: hit_tri(R, slot, o, d, prev, b); break;
+    case RT_PRIM_SPHERE: hit_sph(R, slot, o, d, prev, xf, b); break;
+    default: hit_plane(R, slot, o, d, prev, b); break;
+    }
+}
+
 
 // One visit of a 4-wide quantised node (Node4Q): slab tests of the four children against
 // dequantised planes t = q * (2^e / d) + (origin - o) / d, nearest hit child next, the other hit
@@ -730,12 +745,12 @@ __device__ __forceinline__ void flush_counts(const Lane& L, const Counters& cnt,
 
 // Brute-force megakernel: every loop iteration issues one closest-hit query per live lane
 // (the scene's records arrive through scalar loads) and shades it.
-template <bool LDS, bool STATS>
+template <bool CULL, bool LDS, bool STATS>
 __global__ void __launch_bounds__(256, RT_PATH_WAVES)
     path_kernel(PathScene s, CameraF cam, PathParams p, const TestRec* __restrict__ tests,
                 const RectRec* __restrict__ rects, const PrimF* __restrict__ prims_g, const NodeF* __restrict__ nodes,
-                const Node4Q* __restrict__ nodes4, const XformF* __restrict__ xf, const MatF* __restrict__ mats_g,
-                const float4* __restrict__ vnormals)
+                const Node4Q* __restrict__ nodes4, const GroupRec* __restrict__ groups, const XformF* __restrict__ xf,
+                const MatF* __restrict__ mats_g, const float4* __restrict__ vnormals)
 {
     extern __shared__ float4 lds_scene[];
     const ShadeRecs R = stage_scene<LDS>(s, prims_g, mats_g, xf, lds_scene);
@@ -769,15 +784,13 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
 #ifdef RT_EXP_DUP_TRACE // cost experiment: a second closest-hit query from a perturbed origin
             {
                 Best b2{__builtin_huge_valf(), -1, 0.0f, 0.0f};
-                trace_brute(s, tests, rects, xf, S.o + v3(exp_sink * 1e-30f, 0, 0), S.d, S.prev, b2);
+                unsigned u0 = 0, u1 = 0;
+            trace_brute<CULL, false>(s, groups, tests, rects, xf, S.o + v3(exp_sink * 1e-30f, 0, 0), S.d, S.prev, b2,
+                                     u0, u1);
                 exp_sink += b2.t;
             }
 #endif
-            trace_brute(s, tests, rects, xf, S.o, S.d, S.prev, b);
-            if (STATS) {
-                cnt.tris += s.n_rect[0] + s.n_rect[1] + s.n_rect[2] + s.n_tri;
-                cnt.sphs += s.n_sph;
-            }
+            trace_brute<CULL, STATS>(s, groups, tests, rects, xf, S.o, S.d, S.prev, b, cnt.tris, cnt.sphs);
             for (int i = pln0; i < pln0 + s.n_pln; i++) hit_plane(tests[i], i, S.o, S.d, S.prev, b);
             if (STATS) t2 = __builtin_readcyclecounter();
 #ifdef RT_EXP_DUP_SHADE // cost experiment: a second bounce on a copy
@@ -814,7 +827,8 @@ template <int WIDTH, int STACK, bool LDS, bool STATS>
 __global__ void __launch_bounds__(256, RT_BVH_WAVES)
     path_kernel_bvh(PathScene s, CameraF cam, PathParams p, const TestRec* __restrict__ tests,
                     const RectRec* __restrict__ rects, const PrimF* __restrict__ prims_g,
-                    const NodeF* __restrict__ nodes, const Node4Q* __restrict__ nodes4, const XformF* __restrict__ xf,
+                    const NodeF* __restrict__ nodes, const Node4Q* __restrict__ nodes4,
+                    const GroupRec* __restrict__ groups, const XformF* __restrict__ xf,
                     const MatF* __restrict__ mats_g, const float4* __restrict__ vnormals)
 {
     __shared__ int stack_mem[STACK * 256];
@@ -1007,12 +1021,12 @@ __global__ void colors_1spp_kernel(PathParams p, double* out)
 }
 
 using PathKernel = void (*)(PathScene, CameraF, PathParams, const TestRec*, const RectRec*, const PrimF*,
-                            const NodeF*, const Node4Q*, const XformF*, const MatF*, const float4*);
+                            const NodeF*, const Node4Q*, const GroupRec*, const XformF*, const MatF*, const float4*);
 
-template <bool LDS>
+template <bool CULL, bool LDS>
 PathKernel pick_brute(bool stats)
 {
-    return stats ? path_kernel<LDS, true> : path_kernel<LDS, false>;
+    return stats ? path_kernel<CULL, LDS, true> : path_kernel<CULL, LDS, false>;
 }
 template <int WIDTH, int STACK, bool LDS>
 PathKernel pick_bvh(bool stats)
@@ -1020,22 +1034,25 @@ PathKernel pick_bvh(bool stats)
     return stats ? path_kernel_bvh<WIDTH, STACK, LDS, true> : path_kernel_bvh<WIDTH, STACK, LDS, false>;
 }
 
-// variant = kernel * 2 + lds; kernel 0 brute force, 1/2 BVH2 (24/48-entry stack), 3/4/5 wide BVH (32/40/64)
+// variant = kernel * 2 + lds; kernel 0 brute force (flat), 1 brute force (grouped, culled),
+// 2/3 BVH2 (24/48-entry stack), 4/5/6 wide BVH (32/40/64)
 PathKernel pick(int variant, bool stats)
 {
     switch (variant) {
-    case 1: return pick_brute<true>(stats);
-    case 2: return pick_bvh<2, 24, false>(stats);
-    case 3: return pick_bvh<2, 24, true>(stats);
-    case 4: return pick_bvh<2, 48, false>(stats);
-    case 5: return pick_bvh<2, 48, true>(stats);
-    case 6: return pick_bvh<4, 32, false>(stats);
-    case 7: return pick_bvh<4, 32, true>(stats);
-    case 8: return pick_bvh<4, 40, false>(stats);
-    case 9: return pick_bvh<4, 40, true>(stats);
-    case 10: return pick_bvh<4, 64, false>(stats);
-    case 11: return pick_bvh<4, 64, true>(stats);
-    default: return pick_brute<false>(stats);
+    case 1: return pick_brute<false, true>(stats);
+    case 2: return pick_brute<true, false>(stats);
+    case 3: return pick_brute<true, true>(stats);
+    case 4: return pick_bvh<2, 24, false>(stats);
+    case 5: return pick_bvh<2, 24, true>(stats);
+    case 6: return pick_bvh<2, 48, false>(stats);
+    case 7: return pick_bvh<2, 48, true>(stats);
+    case 8: return pick_bvh<4, 32, false>(stats);
+    case 9: return pick_bvh<4, 32, true>(stats);
+    case 10: return pick_bvh<4, 40, false>(stats);
+    case 11: return pick_bvh<4, 40, true>(stats);
+    case 12: return pick_bvh<4, 64, false>(stats);
+    case 13: return pick_bvh<4, 64, true>(stats);
+    default: return pick_brute<false, false>(stats);
     }
 }
 
@@ -1086,19 +1103,22 @@ hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& 
                        hipStream_t stream, bool stats)
 {
     PathScene ps = make_path_scene(s);
-    if (variant >= 6) ps.root = s.root4; // the wide kernels walk the collapsed tree
+    const int kernel = variant >> 1;
+    if (kernel >= 4) ps.root = s.root4; // the wide kernels walk the collapsed tree
+    const bool grouped = kernel == 1, bvh = kernel >= 2;
+    ps.n_groups = grouped ? s.n_groups_gr : 1;
     CameraF ca = cam;
     PathParams pa = p;
-    const bool bvh = variant >= 2;
-    const TestRec* tests = bvh ? s.tests_bvh : s.tests_bf;
-    const RectRec* rects = s.rects_bf;
-    const PrimF* prims = bvh ? s.prims_bvh : s.prims_bf;
+    const TestRec* tests = bvh ? s.tests_bvh : grouped ? s.tests_gr : s.tests_bf;
+    const RectRec* rects = grouped ? s.rects_gr : s.rects_bf;
+    const PrimF* prims = bvh ? s.prims_bvh : grouped ? s.prims_gr : s.prims_bf;
     const NodeF* nodes = s.nodes;
     const Node4Q* nodes4 = s.nodes4;
+    const GroupRec* groups = grouped ? s.groups_gr : s.groups_bf;
     const XformF* xf = s.xf;
     const MatF* mats = s.mats;
     const float4* vn = s.vnormals;
-    void* args[] = {&ps, &ca, &pa, &tests, &rects, &prims, &nodes, &nodes4, &xf, &mats, &vn};
+    void* args[] = {&ps, &ca, &pa, &tests, &rects, &prims, &nodes, &nodes4, &groups, &xf, &mats, &vn};
     const size_t dyn = (variant & 1) ? path_lds_bytes(s) : 0;
     return hipLaunchKernel(reinterpret_cast<const void*>(pick(variant, stats)), dim3(grid_blocks), dim3(256), args, dyn,
                            stream);

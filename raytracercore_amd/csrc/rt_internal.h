@@ -92,6 +92,17 @@ struct alignas(16) MatF {       // per primitive ID, 80 B
     float pad;
 };
 
+// A group of the brute-force slot order (48 B): its primitives' box (fp32, rounded outward) and
+// typed ranges -- rects (x | y | z) in RectRec order from rect_first, then triangles and spheres
+// in slot order from tri_slot.  The grouped kernel skips a group when no lane of the wave meets
+// its box; the flat order is one group whose box is never tested.
+struct alignas(16) GroupRec {
+    float4 lo;     // xyz, w = bitcast rect_first
+    float4 hi;     // xyz, w = bitcast tri_slot
+    int32_t n_rect[3];
+    int32_t n_tri_sph; // n_tri | n_sph << 16
+};
+
 // Intersection record of the fp32 kernel (64 B), one per primitive slot:
 //   triangle: rows r0..r2 of the affine inverse of [e01 e02 n | v0], so that
 //             (u, v, w) = M (p, 1): w = 0 on the plane, (u, v) = the barycentrics the
@@ -113,6 +124,7 @@ struct PathScene {
     int32_t n_slots;             // n_bvh + n_pln (PrimF records)
     int32_t n_ids;               // primitive IDs (MatF records)
     int32_t n_xf;                // XformF records
+    int32_t n_groups;            // brute force: GroupRec records
     int32_t root;                // child reference of the BVH root
     int32_t width;               // frame width (RNG pixel index)
     int32_t recursion;
@@ -161,6 +173,13 @@ struct DevScene {
     const TestRec* tests_bf;
     const RectRec* rects_bf;    // slots [0, n_rect[0] + n_rect[1] + n_rect[2])
     const PrimF* prims_bf;
+    const GroupRec* groups_bf;  // one group: the whole flat order
+    // the grouped brute-force order (same records, group-major slot order)
+    const TestRec* tests_gr;
+    const RectRec* rects_gr;
+    const PrimF* prims_gr;
+    const GroupRec* groups_gr;
+    int32_t n_groups_gr;
     int32_t n_rect[3];
     int32_t n_tri, n_sph, n_pln; // n_tri counts general triangles only
     const TestRec* tests_bvh;

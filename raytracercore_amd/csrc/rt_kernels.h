@@ -32,7 +32,8 @@ struct PathParams {
 hipError_t launch_primary_ids(const DevScene& s, const CameraD& cam, int x0, int y0, int w, int h, int mode,
                               int32_t* d_ids, hipStream_t stream);
 
-// Kernel variant: kernel 0 brute force, 1/2 BVH2 (24/48-entry stack), 3/4/5 wide BVH (32/40/64);
+// Kernel variant: kernel 0 brute force, 1 grouped brute force, 2/3 BVH2 (24/48-entry stack),
+// 4/5/6 wide BVH (32/40/64);
 // lds stages the shading records in LDS.
 int path_variant(int kernel, bool lds);
 size_t path_lds_bytes(const DevScene& s);   // dynamic LDS of the staged (lds) variants

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <string>
 #include <thread>
@@ -96,6 +97,12 @@ struct rt_scene {
     DevBuf<PrimF> prims_bf, prims_bvh;
     DevBuf<TestRec> tests_bf, tests_bvh;
     DevBuf<RectRec> rects_bf;
+    DevBuf<GroupRec> groups_bf;
+    DevBuf<PrimF> prims_gr;
+    DevBuf<TestRec> tests_gr;
+    DevBuf<RectRec> rects_gr;
+    DevBuf<GroupRec> groups_gr;
+    double grouped_measured = 0; // calibrated brute-force cost ratio flat / grouped (AUTO picks grouped above 1.25)
     DevBuf<NodeF> nodes;
     DevBuf<Node4Q> nodes4;
     DevBuf<XformF> xf;
@@ -266,31 +273,120 @@ int upload_scene(rt_scene* s)
         r.sg = 0; // set once the slot is known
         return r;
     };
-    std::vector<PrimF> bf, bv;
-    std::vector<TestRec> tbf, tbv;
-    std::vector<RectRec> rects;
-    int nr[3] = {0, 0, 0}, nt = 0, ns = 0, np = 0;
-    std::vector<int> group(n);
+    // Brute-force slot orders: groups of primitives, each [x-rects | y-rects | z-rects | triangles |
+    // spheres], then the planes.  The flat order is one group of everything; the grouped order
+    // cuts the SAH BVH into subtrees of at most kGroupMax primitives.
+    struct BruteOrder {
+        std::vector<PrimF> prims;
+        std::vector<TestRec> tests;
+        std::vector<RectRec> rects;
+        std::vector<GroupRec> groups;
+        int nr[3] = {0, 0, 0}, nt = 0, ns = 0;
+    };
+    std::vector<int> kind_of(n);
     for (int i = 0; i < n; i++) {
         const int ax = rect_axis(i);
-        group[i] = ax >= 0 ? ax : (H[i].kind == RT_PRIM_TRIANGLE ? 3 : H[i].kind == RT_PRIM_SPHERE ? 4 : 5);
+        kind_of[i] = ax >= 0 ? ax : (H[i].kind == RT_PRIM_TRIANGLE ? 3 : H[i].kind == RT_PRIM_SPHERE ? 4 : 5);
     }
-    for (int g = 0; g < 6; g++)
-        for (int i = 0; i < n; i++) {
-            if (group[i] != g) continue;
-            PrimF f = primf(i);
-            if (g < 3) {
-                const uint32_t fl = p_flags_with_axis(H[i].flags, g);
-                std::memcpy(&f.b.w, &fl, 4);
-                rects.push_back(rectrec(i, g));
-                rects.back().sg = (int)bf.size() << 1;
-                nr[g]++;
-            } else {
-                (g == 3 ? nt : g == 4 ? ns : np)++;
-            }
-            bf.push_back(f);
-            tbf.push_back(testrec(i));
+    auto fbox = [&](const std::vector<int>& ids, float lo[3], float hi[3]) {
+        for (int k = 0; k < 3; k++) {
+            lo[k] = __builtin_huge_valf();
+            hi[k] = -__builtin_huge_valf();
         }
+        for (int i : ids) {
+            const double l[3] = {H[i].box.mn.x, H[i].box.mn.y, H[i].box.mn.z};
+            const double u[3] = {H[i].box.mx.x, H[i].box.mx.y, H[i].box.mx.z};
+            for (int k = 0; k < 3; k++) {
+                const double pad = (std::fabs(l[k]) + std::fabs(u[k])) * 9.5367431640625e-07 + 1e-30;
+                lo[k] = std::min(lo[k], std::nextafter((float)(l[k] - pad), -__builtin_huge_valf()));
+                hi[k] = std::max(hi[k], std::nextafter((float)(u[k] + pad), __builtin_huge_valf()));
+            }
+        }
+    };
+    auto build_order = [&](const std::vector<std::vector<int>>& groups) {
+        BruteOrder o;
+        for (const auto& g : groups) {
+            GroupRec G;
+            std::memset(&G, 0, sizeof G);
+            float lo[3], hi[3];
+            fbox(g, lo, hi);
+            const int rect_first = (int)o.rects.size();
+            int cnt[5] = {0, 0, 0, 0, 0};
+            int tri_slot = 0;
+            for (int kind = 0; kind < 5; kind++) {
+                if (kind == 3) tri_slot = (int)o.prims.size();
+                for (int i : g) {
+                    if (kind_of[i] != kind) continue;
+                    PrimF f = primf(i);
+                    if (kind < 3) {
+                        const uint32_t fl = p_flags_with_axis(H[i].flags, kind);
+                        std::memcpy(&f.b.w, &fl, 4);
+                        o.rects.push_back(rectrec(i, kind));
+                        o.rects.back().sg = (int)o.prims.size() << 1;
+                        o.nr[kind]++;
+                    } else {
+                        (kind == 3 ? o.nt : o.ns)++;
+                    }
+                    cnt[kind]++;
+                    o.prims.push_back(f);
+                    o.tests.push_back(testrec(i));
+                }
+            }
+            G.lo = make_float4(lo[0], lo[1], lo[2], as_f(rect_first));
+            G.hi = make_float4(hi[0], hi[1], hi[2], as_f(tri_slot));
+            for (int k = 0; k < 3; k++) G.n_rect[k] = cnt[k];
+            G.n_tri_sph = cnt[3] | (cnt[4] << 16);
+            o.groups.push_back(G);
+        }
+        for (int i = 0; i < n; i++) // planes follow
+            if (kind_of[i] == 5) {
+                o.prims.push_back(primf(i));
+                o.tests.push_back(testrec(i));
+            }
+        o.tests.push_back(TestRec{}); // spare records: loops may load one past a range
+        o.rects.push_back(RectRec{});
+        return o;
+    };
+    std::vector<int> all;
+    for (int i = 0; i < n; i++)
+        if (kind_of[i] != 5) all.push_back(i);
+    BruteOrder flat = build_order({all});
+    int nr[3] = {flat.nr[0], flat.nr[1], flat.nr[2]}, nt = flat.nt, ns = flat.ns, np = 0;
+    for (int i = 0; i < n; i++) np += kind_of[i] == 5;
+    // groups: subtrees of the SAH BVH with at most kGroupMax primitives (small scenes only)
+    constexpr int kGroupMax = 8;
+    std::vector<std::vector<int>> cut;
+    if ((int)all.size() <= 4096 && !s->sah.order.empty()) {
+        std::function<void(int, std::vector<int>&)> leaves = [&](int ref, std::vector<int>& out) {
+            if (ref < 0) {
+                const int code = ~ref, first = code >> 3, c = (code & 7) + 1;
+                for (int k = first; k < first + c; k++) out.push_back(s->sah.order[k]);
+                return;
+            }
+            int l, r;
+            std::memcpy(&l, &s->sah.nodes[ref].lmin.w, 4);
+            std::memcpy(&r, &s->sah.nodes[ref].rmin.w, 4);
+            leaves(l, out);
+            leaves(r, out);
+        };
+        std::function<void(int)> split = [&](int ref) {
+            std::vector<int> sub;
+            leaves(ref, sub);
+            if ((int)sub.size() <= kGroupMax || ref < 0) {
+                cut.push_back(sub);
+                return;
+            }
+            int l, r;
+            std::memcpy(&l, &s->sah.nodes[ref].lmin.w, 4);
+            std::memcpy(&r, &s->sah.nodes[ref].rmin.w, 4);
+            split(l);
+            split(r);
+        };
+        split(s->sah.root);
+    }
+    BruteOrder grouped = cut.empty() ? BruteOrder{} : build_order(cut);
+    std::vector<PrimF> bv;
+    std::vector<TestRec> tbv;
     for (int i : s->sah.order) {
         bv.push_back(primf(i));
         tbv.push_back(testrec(i));
@@ -318,21 +414,26 @@ int upload_scene(rt_scene* s)
     }
     HIP_TRY(s->prims_d.upload(pd));
     HIP_TRY(s->xf_d.upload(xd));
-    HIP_TRY(s->prims_bf.upload(bf));
+    HIP_TRY(s->prims_bf.upload(flat.prims));
+    HIP_TRY(s->tests_bf.upload(flat.tests));
+    HIP_TRY(s->rects_bf.upload(flat.rects));
+    HIP_TRY(s->groups_bf.upload(flat.groups));
+    HIP_TRY(s->prims_gr.upload(grouped.prims));
+    HIP_TRY(s->tests_gr.upload(grouped.tests));
+    HIP_TRY(s->rects_gr.upload(grouped.rects));
+    HIP_TRY(s->groups_gr.upload(grouped.groups));
     HIP_TRY(s->prims_bvh.upload(bv));
-    tbf.push_back(TestRec{}); // spare records: the brute-force loops prefetch one ahead
-    tbv.push_back(TestRec{});
-    HIP_TRY(s->tests_bf.upload(tbf));
+    tbv.push_back(TestRec{}); // spare record: the BVH leaf step loads one past a leaf
     HIP_TRY(s->tests_bvh.upload(tbv));
-    rects.push_back(RectRec{}); // one spare record: the kernel prefetches one past each group
-    HIP_TRY(s->rects_bf.upload(rects));
     HIP_TRY(s->nodes.upload(s->sah.nodes));
     HIP_TRY(s->nodes4.upload(s->bvh4.nodes));
     HIP_TRY(s->xf.upload(xf));
     HIP_TRY(s->mats.upload(mats));
     HIP_TRY(s->vnormals.upload(vn));
     s->device_bytes = pd.size() * sizeof(PrimD) + xd.size() * sizeof(XformD) +
-                      bf.size() * sizeof(PrimF) + bv.size() * sizeof(PrimF) + s->sah.nodes.size() * sizeof(NodeF) +
+                      (flat.prims.size() + grouped.prims.size() + bv.size()) * sizeof(PrimF) +
+                      (flat.tests.size() + grouped.tests.size() + tbv.size()) * sizeof(TestRec) +
+                      s->sah.nodes.size() * sizeof(NodeF) +
                       s->bvh4.nodes.size() * sizeof(Node4Q) +
                       xf.size() * sizeof(XformF) + mats.size() * sizeof(MatF) + vn.size() * sizeof(float4);
 
@@ -341,6 +442,12 @@ int upload_scene(rt_scene* s)
     d.tests_bvh = s->tests_bvh.p;
     d.rects_bf = s->rects_bf.p;
     d.prims_bf = s->prims_bf.p;
+    d.groups_bf = s->groups_bf.p;
+    d.tests_gr = s->tests_gr.p;
+    d.rects_gr = s->rects_gr.p;
+    d.prims_gr = s->prims_gr.p;
+    d.groups_gr = s->groups_gr.p;
+    d.n_groups_gr = (int)grouped.groups.size();
     for (int k = 0; k < 3; k++) d.n_rect[k] = nr[k];
     d.n_tri = nt;
     d.n_sph = ns;
@@ -394,20 +501,24 @@ int resolve_traversal(rt_scene* s)
         const int n_bvh = s->dev.n_rect[0] + s->dev.n_rect[1] + s->dev.n_rect[2] + s->dev.n_tri + s->dev.n_sph;
         t = n_bvh <= 48 ? RT_TRAVERSAL_BRUTE : RT_TRAVERSAL_BVH;
     }
-    // kernel: 0 brute force, 1/2 BVH2 with a 24/48-entry stack, 3/4/5 wide BVH with 32/40/64
-    int kernel = 0;
+    if (s->traversal == RT_TRAVERSAL_AUTO && t == RT_TRAVERSAL_BRUTE && s->grouped_measured > 1.25)
+        t = RT_TRAVERSAL_GROUPED;
+    if (t == RT_TRAVERSAL_GROUPED && s->dev.n_groups_gr == 0) t = RT_TRAVERSAL_BRUTE; // too big to group
+    // kernel: 0 brute force, 1 grouped brute force, 2/3 BVH2 with a 24/48-entry stack,
+    // 4/5/6 wide BVH with 32/40/64
+    int kernel = t == RT_TRAVERSAL_GROUPED ? 1 : 0;
     if (t == RT_TRAVERSAL_BVH2) {
         if (s->sah.depth >= 48) {
             set_error("BVH2 deeper than the kernel's LDS stack");
             return RT_ERR_ARG;
         }
-        kernel = s->sah.depth < 24 ? 1 : 2;
+        kernel = s->sah.depth < 24 ? 2 : 3;
     } else if (t == RT_TRAVERSAL_BVH) {
         if (s->bvh4.stack_need > 64) {
             set_error("wide BVH needs a deeper traversal stack than the kernel's 64 entries");
             return RT_ERR_ARG;
         }
-        kernel = s->bvh4.stack_need <= 32 ? 3 : s->bvh4.stack_need <= 40 ? 4 : 5;
+        kernel = s->bvh4.stack_need <= 32 ? 4 : s->bvh4.stack_need <= 40 ? 5 : 6;
     }
     s->resolved = t;
     // Stage the shading records in LDS when that costs no occupancy (RTCORE_PATH_LDS=0/1 forces
@@ -422,6 +533,56 @@ int resolve_traversal(rt_scene* s)
     s->blocks_per_cu = use_lds ? occ_staged : occ_plain;
     if (s->stats_on) s->stats_blocks_per_cu = path_blocks_per_cu(s->variant, lds, true);
     return RT_OK;
+}
+
+PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint64_t seed, uint64_t base);
+int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t stream);
+
+// AUTO on a small scene: flat or grouped brute force?  Whether a group can be skipped depends on
+// how coherent a wave's rays are, which the camera decides, so each camera is calibrated once:
+// the grouped kernel's instrumented variant renders a fixed 64x64 tile at 2 spp and counts the
+// primitive tests it actually made.  The choice is a function of scene, camera and that fixed
+// sample only (no timing), so it is the same on every run.
+int calibrate_grouping(rt_scene* s)
+{
+    s->grouped_measured = 0;
+    if (s->traversal != RT_TRAVERSAL_AUTO || s->dev.n_groups_gr < 2) return RT_OK;
+    const int n_bvh = s->dev.n_rect[0] + s->dev.n_rect[1] + s->dev.n_rect[2] + s->dev.n_tri + s->dev.n_sph;
+    if (n_bvh > 48) return RT_OK;
+    const int w = std::min(64, s->params.width), h = std::min(64, s->params.height);
+    const int x0 = (s->params.width - w) / 2, y0 = (s->params.height - h) / 2;
+    const int saved_variant = s->variant, saved_blocks = s->blocks_per_cu;
+    const int variant = path_variant(1, false);
+    s->variant = variant;
+    s->blocks_per_cu = path_blocks_per_cu(variant, 0, true);
+    HIP_TRY(s->stats_buf.reserve(RT_STATS_COUNT));
+    HIP_TRY(s->sum.reserve((size_t)3 * w * h));
+    HIP_TRY(s->samples.reserve((size_t)w * h));
+    HIP_TRY(s->misses.reserve((size_t)w * h));
+    HIP_TRY(hipMemsetAsync(s->stats_buf.p, 0, RT_STATS_COUNT * sizeof(unsigned long long), s->stream));
+    HIP_TRY(hipMemsetAsync(s->rays.p, 0, sizeof(unsigned long long), s->stream));
+    const bool was_on = s->stats_on;
+    const int was_blocks = s->stats_blocks_per_cu;
+    s->stats_on = true;
+    s->stats_blocks_per_cu = s->blocks_per_cu;
+    PathParams p = make_params(s, x0, y0, w, h, 2, 0x5EEDull, 0);
+    int rc = run_path(s, p, s->rays.p, s->stream);
+    s->stats_on = was_on;
+    s->stats_blocks_per_cu = was_blocks;
+    s->variant = saved_variant;
+    s->blocks_per_cu = saved_blocks;
+    if (rc != RT_OK) return rc;
+    unsigned long long st[RT_STATS_COUNT], rays = 0;
+    HIP_TRY(hipMemcpyAsync(st, s->stats_buf.p, sizeof st, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipMemcpyAsync(&rays, s->rays.p, sizeof rays, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    HIP_TRY(hipMemsetAsync(s->stats_buf.p, 0, RT_STATS_COUNT * sizeof(unsigned long long), s->stream));
+    if (rays == 0) return RT_OK;
+    // relative costs of a rect/triangle test, a sphere test and a group box test (instruction counts)
+    const double flat = 20.0 * (n_bvh - s->dev.n_sph) + 30.0 * s->dev.n_sph;
+    const double grouped = 15.0 * s->dev.n_groups_gr + (20.0 * st[1] + 30.0 * st[2]) / (double)rays;
+    s->grouped_measured = flat / std::max(grouped, 1e-9);
+    return resolve_traversal(s);
 }
 
 PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint64_t seed, uint64_t base)
@@ -570,17 +731,19 @@ int rt_scene_set_camera(rt_scene* s, const rt_camera* cam)
     }
     camera_init(*cam, s->params.width, s->params.height, s->camd, s->camf);
     s->has_camera = true;
-    return RT_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    return calibrate_grouping(s);
 }
 
 int rt_scene_set_traversal(rt_scene* s, int32_t traversal)
 {
-    if (!s || traversal < RT_TRAVERSAL_AUTO || traversal > RT_TRAVERSAL_BVH2) {
+    if (!s || traversal < RT_TRAVERSAL_AUTO || traversal > RT_TRAVERSAL_GROUPED) {
         set_error("rt_scene_set_traversal: bad argument");
         return RT_ERR_ARG;
     }
     HIP_TRY(hipSetDevice(s->device));
     s->traversal = traversal;
+    if (traversal == RT_TRAVERSAL_AUTO && s->has_camera) return calibrate_grouping(s);
     return resolve_traversal(s);
 }
 

@@ -159,7 +159,7 @@ def test_sample_ranges_compose(rc, scenes):
     assert np.allclose(s1 + s2, s, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("mode", ["BVH", "BVH2"])
+@pytest.mark.parametrize("mode", ["BVH", "BVH2", "GROUPED"])
 @pytest.mark.parametrize("name", ["die.txt", "bounce.txt"])
 def test_traversal_modes_agree(rc, scenes, name, mode):
     """Brute force and BVH traversal (wide and binary) return the same closest hits."""
@@ -173,7 +173,7 @@ def test_traversal_modes_agree(rc, scenes, name, mode):
     assert np.allclose(sa, sb, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("mode", ["BVH", "BVH2"])
+@pytest.mark.parametrize("mode", ["BVH", "BVH2", "GROUPED"])
 def test_traversal_modes_agree_mesh(rc, mode):
     """The same on a small procedural height field (3,200 triangles): BVH == brute force up to
     ties on shared triangle edges."""
