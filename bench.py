@@ -30,6 +30,8 @@ CONFIGS = {
     "bounce256": ("bounce.txt", 0, 256, 256, 16),
     # C4: procedural 1M-triangle height field in the bounce room (raytracercore_amd/scenes.py)
     "mesh1080": ("@mesh", 0, 1920, 1080, 64),
+    # C5: die.txt at 4K, 4096 spp per frame over 8 GPUs = 512 spp per GPU per step (sample-sharded)
+    "die4k": ("die.txt", 0, 3840, 2160, 512),
 }
 
 
