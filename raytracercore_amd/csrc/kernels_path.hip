@@ -432,12 +432,14 @@ __device__ __forceinline__ void start_sample(const CameraF& cam, int x, int y, S
     S.prev = -1;
 }
 
-// 1 - z^2 for z = 2^a (a <= 0) without cancellation: 1 - 2^(2a) = -expm1(2a ln 2)
+// 1 - z^2 for z = 2^a (a <= 0) without cancellation: 1 - 2^(2a) = -expm1(2a ln 2); both forms
+// evaluated and selected (no divergent branch)
 __device__ __forceinline__ float one_minus_exp2_2a(float a)
 {
     const float x = 2.0f * a * 0.69314718055994531f;
-    if (x > -0.0625f) return -x * fmaf(x, fmaf(x, fmaf(x, 1.0f / 24.0f, 1.0f / 6.0f), 0.5f), 1.0f);
-    return 1.0f - __builtin_amdgcn_exp2f(2.0f * a);
+    const float series = -x * fmaf(x, fmaf(x, fmaf(x, 1.0f / 24.0f, 1.0f / 6.0f), 0.5f), 1.0f);
+    const float direct = 1.0f - __builtin_amdgcn_exp2f(2.0f * a);
+    return x > -0.0625f ? series : direct;
 }
 
 // One bounce of Raytracer.GetColor after the closest-hit query.  Returns 0 to continue the
@@ -466,54 +468,39 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
         col = S.tint * emis;
         return 1;
     }
-    // hit position and normal facing the incoming ray
-    V3 pos, nrm;
-    if (kind == RT_PRIM_TRIANGLE) {
-        const uint32_t axis = (fl & F_AXIS_MASK) >> F_AXIS_SHIFT;
-        if (axis) { // axis-aligned rectangle hit (hit_rect): on the plane through Vert0
-            gin = dot(S.d, xyz(P.d)) > 0.0f; // Moller-Trumbore's inside = d . N > 0
-            pos = madd(S.d, b.t, S.o);
-            if (axis == 1) pos.x = P.a.x;
-            else if (axis == 2) pos.y = P.a.y;
-            else pos.z = P.a.z;
-        } else {
-            pos = madd(xyz(P.b), b.u, madd(xyz(P.c), b.v, xyz(P.a)));
-        }
-        if (fl & F_HASNORMALS) { // Triangle.GetNormal quirk: Normal is never set -> NaN when inside
+    // hit position and normal facing the incoming ray: one straight-line form for every kind
+    // (world point o + t d; flat kinds carry their face normal in P.d, spheres 1/r in P.b.y), with
+    // transformed spheres and vertex-normal triangles on a separate (rare) path
+    V3 pos = madd(S.d, b.t, S.o);
+    const bool sph = kind == RT_PRIM_SPHERE;
+    const uint32_t axis = (fl & F_AXIS_MASK) >> F_AXIS_SHIFT; // axis-aligned rectangle: on its plane
+    if (axis) gin = dot(S.d, xyz(P.d)) > 0.0f;                 // Moller-Trumbore's inside = d . N > 0
+    pos.x = axis == 1 ? P.a.x : pos.x;
+    pos.y = axis == 2 ? P.a.y : pos.y;
+    pos.z = axis == 3 ? P.a.z : pos.z;
+    V3 n = sph ? (pos - xyz(P.a)) * P.b.y : xyz(P.d);
+    if (fl & (F_TRANSFORMED | F_HASNORMALS)) {
+        if (sph) { // ellipsoid: the hit in object space (b.u is the object-space distance)
+            const XformF& X = xfs[__float_as_int(P.b.z)];
+            const V3 oo = xf_point(X.to_world, S.o);
+            const V3 dd = normalize(xf_dir(X.to_world, S.d));
+            const V3 op = madd(dd, b.u, oo);
+            pos = xf_point(X.to_obj, op);
+            n = normalize(xf_dir(X.to_normal, (op - xyz(P.a)) * P.b.y));
+        } else { // Triangle.GetNormal quirk: Normal is never set -> NaN when inside
             const float4* vn = vnormals + 3 * id;
-            nrm = normalize(madd(xyz(vn[2]), b.u + b.v, madd(xyz(vn[1]), b.v, xyz(vn[0]) * b.u)));
-            if (gin) nrm = v3(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
-        } else {
-            nrm = gin ? -xyz(P.d) : xyz(P.d);
+            n = normalize(madd(xyz(vn[2]), b.u + b.v, madd(xyz(vn[1]), b.v, xyz(vn[0]) * b.u)));
+            if (gin) n = v3(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
         }
-    } else if (kind == RT_PRIM_SPHERE) {
-        V3 oo = S.o, dd = S.d;
-        const bool tr = (fl & F_TRANSFORMED) != 0;
-        const XformF* X = tr ? &xfs[__float_as_int(P.b.z)] : nullptr;
-        if (tr) {
-            oo = xf_point(X->to_world, S.o);
-            dd = normalize(xf_dir(X->to_world, S.d));
-        }
-        const V3 op = madd(dd, b.u, oo);
-        V3 n = (op - xyz(P.a)) * rcp(P.b.x);
-        if (tr) {
-            pos = xf_point(X->to_obj, op);
-            n = normalize(xf_dir(X->to_normal, n));
-        } else {
-            pos = op;
-        }
-        nrm = gin ? -n : n;
-    } else {
-        pos = madd(S.d, b.u, S.o);
-        nrm = gin ? -xyz(P.a) : xyz(P.a);
     }
+    const V3 nrm = gin ? -n : n;
     const bool inside = gin ^ ((fl & F_INVERT) != 0);
 
     // RandomShine (Raytracer.cs:51-56): z = U^(1/shininess), theta = U * 2pi
     const float shin = M.shininess;
     float z = 1.0f, sz = 0.0f;
     if (!(__builtin_isinf(shin) && shin > 0.0f)) {
-        const float a = __builtin_amdgcn_logf(next_u(S.rng)) * rcp(shin); // log2(U) / shininess
+        const float a = __builtin_amdgcn_logf(next_u(S.rng)) * M.inv_shininess; // log2(U) / shininess
         z = __builtin_amdgcn_exp2f(a);
         sz = fsqrt(one_minus_exp2_2a(a));
     }

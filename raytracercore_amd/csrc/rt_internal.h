@@ -70,9 +70,9 @@ struct alignas(16) RefNode {    // 80 B, depth-first pre-order; left child = thi
 // ---- fast fp32 scene (path tracing) --------------------------------------------------
 struct alignas(16) PrimF {      // 64 B
     float4 a; // tri: v0.xyz, id | sphere: c.xyz, id | plane: N.xyz, id
-    float4 b; // tri: e01.xyz, flags | sphere: (r, r^2, xf, flags) | plane: (dist, 0, 0, flags)
+    float4 b; // tri: e01.xyz, flags | sphere: (r, 1/r, xf, flags) | plane: (dist, 0, 0, flags)
     float4 c; // tri: e02.xyz, 0
-    float4 d; // tri: N.xyz, 0
+    float4 d; // tri and plane: N.xyz, 0
 };
 
 struct alignas(16) XformF {     // rows 0-2 of each 4x4 (last row is 0 0 0 1)
@@ -89,7 +89,7 @@ struct alignas(16) MatF {       // per primitive ID, 80 B
     float shininess;            // may be +inf
     float ior;                  // RefractiveIndex
     uint32_t flags;
-    float pad;
+    float inv_shininess;        // 1 / Shininess (RandomShine's exponent)
 };
 
 // A group of the brute-force slot order (48 B): its primitives' box (fp32, rounded outward) and

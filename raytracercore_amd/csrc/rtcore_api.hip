@@ -202,10 +202,11 @@ int upload_scene(rt_scene* s)
             f.d = f4(p.n, 0.0f);
         } else if (p.kind == RT_PRIM_SPHERE) {
             f.a = f4(p.center, as_f(i));
-            f.b = make_float4((float)p.radius, (float)p.radius_sqr, as_f(xf_index[i]), as_f(p.flags));
+            f.b = make_float4((float)p.radius, (float)(1.0 / p.radius), as_f(xf_index[i]), as_f(p.flags));
         } else {
             f.a = f4(p.pn, as_f(i));
             f.b = make_float4((float)p.pd, 0.0f, 0.0f, as_f(p.flags));
+            f.d = f4(p.pn, 0.0f); // face normal where the shading step reads it for every flat kind
         }
         return f;
     };
@@ -410,7 +411,7 @@ int upload_scene(rt_scene* s)
         m.shininess = (float)p.shininess;
         m.ior = (float)p.ior;
         m.flags = p.flags;
-        m.pad = 0;
+        m.inv_shininess = (float)(1.0 / p.shininess);
     }
     HIP_TRY(s->prims_d.upload(pd));
     HIP_TRY(s->xf_d.upload(xd));
