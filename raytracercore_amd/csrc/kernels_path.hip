@@ -534,27 +534,32 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
         col = S.tint * emis;
         return 1;
     }
+    // the choice (Raytracer.cs:177-229): refraction -> specular -> diffuse -> emission, by
+    // subtracting luminances from U * total; then one direction formula per kind of event
     float ray_rand = next_u(S.rng) * total;
-    V3 out_dir;
-    V3 new_tint;
-    if (refr_lum != 0.0f && (ray_rand -= refr_lum) <= 0.0f) { // transmission
-        out_dir = madd(madd(rough, cs, S.d), ior_ratio, rough * (-cos_out));
-        new_tint = inside ? v3(1.0f, 1.0f, 1.0f) : xyz(M.refraction);
-    } else if (spec_lum != 0.0f && (ray_rand -= spec_lum) <= 0.0f) { // specular
-        out_dir = madd(rough, 2.0f * cs, S.d);
-        if (!(dot(out_dir, nrm) > 0.0f)) {
-            col = S.tint * emis;
-            return 1;
-        }
-        new_tint = xyz(M.specular);
-    } else if (diff_lum != 0.0f && (ray_rand -= diff_lum) <= 0.0f) { // diffuse
+    const bool transmit = refr_lum != 0.0f && (ray_rand -= refr_lum) <= 0.0f;
+    const bool specular = !transmit && spec_lum != 0.0f && (ray_rand -= spec_lum) <= 0.0f;
+    const bool diffuse = !transmit && !specular && diff_lum != 0.0f && (ray_rand -= diff_lum) <= 0.0f;
+    if (!(transmit | specular | diffuse)) { // emission
+        col = S.tint * emis;
+        return 1;
+    }
+    V3 out_dir, new_tint;
+    if (diffuse) {
         const float dz = acos_turn2(next_u(S.rng)); // 2 acos(U) / pi (Raytracer.cs:215)
         const float ds = fsqrt(fmaxf(0.0f, 1.0f - dz * dz));
         out_dir = horizon(fr, nrm, dz, ds, next_u(S.rng));
         new_tint = xyz(M.diffuse);
-    } else { // emission
-        col = S.tint * emis;
-        return 1;
+    } else {
+        // transmission: (d + rough cs) eta - rough cos_out; reflection: d + rough 2 cs
+        const float al = transmit ? ior_ratio : 1.0f;
+        const float be = transmit ? cs * ior_ratio - cos_out : 2.0f * cs;
+        out_dir = madd(rough, be, S.d * al);
+        if (specular && !(dot(out_dir, nrm) > 0.0f)) { // a specular ray into the surface ends the path
+            col = S.tint * emis;
+            return 1;
+        }
+        new_tint = transmit ? (inside ? v3(1.0f, 1.0f, 1.0f) : xyz(M.refraction)) : xyz(M.specular);
     }
     S.o = pos;
     S.d = normalize(out_dir);
