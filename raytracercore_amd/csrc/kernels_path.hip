@@ -398,8 +398,8 @@ __device__ __forceinline__ Ray3 camera_ray(const CameraF& c, float x, float y)
 {
     Ray3 r;
     if (c.kind == RT_CAMERA_FRUSTUM) {
-        const float ox = c.tan_x * ((x - c.w2) * rcp(c.w2));
-        const float oy = c.tan_y * ((y - c.h2) * rcp(c.h2));
+        const float ox = fmaf(x, c.tan_x_per_px, -c.tan_x); // tan_x * (x - w2) / w2
+        const float oy = fmaf(y, c.tan_y_per_px, -c.tan_y);
         r.d = normalize(madd(xyz(c.up), oy, madd(xyz(c.side), ox, xyz(c.look))));
         r.o = xyz(c.position);
     } else {

@@ -156,6 +156,7 @@ struct alignas(16) Node4Q {
 struct CameraF {                // post-InitRender state in fp32 (path kernel)
     float4 position, look, side, up;
     float w2, h2, tan_x, tan_y, h_mult, v_mult, image_plane, dof, focal_length;
+    float tan_x_per_px, tan_y_per_px; // tan_x / w2, tan_y / h2 (frustum: ox = x * this - tan_x)
     int32_t kind;
 };
 

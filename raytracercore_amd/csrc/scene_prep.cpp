@@ -165,6 +165,8 @@ void camera_init(const rt_camera& c, int w, int h, CameraD& d, CameraF& f)
     f.h2 = (float)h2;
     f.tan_x = (float)d.tan_x;
     f.tan_y = (float)d.tan_y;
+    f.tan_x_per_px = (float)(d.tan_x / w2);
+    f.tan_y_per_px = (float)(d.tan_y / h2);
     f.h_mult = (float)d.h_mult;
     f.v_mult = (float)d.v_mult;
     f.image_plane = (float)d.image_plane;
