@@ -278,9 +278,32 @@ __device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb)
     db = sw ? t : db;
     rb = sw ? r : rb;
 }
+// Per-lane traversal stack: the first STACK entries in LDS (stride 256 = the block's lanes), deeper
+// entries in a global overflow area (stride = all lanes of the grid), reached only by rare deep
+// paths; the host bounds the depth any ray can need by STACK + RT_STACK_OVF.
+#define RT_STACK_OVF 40
+struct TravStack {
+    int* lds;
+    int* ovf;
+    int ovf_stride;
+};
 template <int STACK>
-__device__ __forceinline__ void wide_visit(const Node4Q& q, V3 id, V3 oi, float best, int& ref, int& sp, int* stk,
-                                           bool& pop)
+__device__ __forceinline__ void push(const TravStack& st, int& sp, int v)
+{
+    if (sp < STACK) st.lds[sp * 256] = v;
+    else st.ovf[(sp - STACK) * st.ovf_stride] = v;
+    sp++;
+}
+template <int STACK>
+__device__ __forceinline__ int pop_ref(const TravStack& st, int& sp)
+{
+    --sp;
+    return sp < STACK ? st.lds[sp * 256] : st.ovf[(sp - STACK) * st.ovf_stride];
+}
+
+template <int STACK>
+__device__ __forceinline__ void wide_visit(const Node4Q& q, V3 id, V3 oi, float best, int& ref, int& sp,
+                                           const TravStack& stk, bool& pop)
 {
     const uint32_t ex = __float_as_uint(q.a.w);
     const float ax = __builtin_amdgcn_ldexpf(id.x, (int)(ex & 255u) - 128);
@@ -318,9 +341,9 @@ __device__ __forceinline__ void wide_visit(const Node4Q& q, V3 id, V3 oi, float 
     cswap(d1, r1, d2, r2);
     const float inf = __builtin_huge_valf();
     if (d0 < inf) {
-        if (d3 < inf && sp < STACK) stk[(sp++) * 256] = r3; // host guarantees the stack depth
-        if (d2 < inf && sp < STACK) stk[(sp++) * 256] = r2;
-        if (d1 < inf && sp < STACK) stk[(sp++) * 256] = r1;
+        if (d3 < inf) push<STACK>(stk, sp, r3);
+        if (d2 < inf) push<STACK>(stk, sp, r2);
+        if (d1 < inf) push<STACK>(stk, sp, r1);
         ref = r0;
         pop = false;
     }
@@ -693,14 +716,12 @@ __device__ __forceinline__ void bounce(Lane& L, Sample& S, const PathScene& s, c
     V3 col;
     const int r = shade(s, R.prims, R.mats, R.xfs, vnormals, b, S, col);
     if (r != 0) {
-        if (r == 1) {
-            L.ar += col.x;
-            L.ag += col.y;
-            L.ab += col.z;
-            L.n_s++;
-        } else {
-            L.n_m++;
-        }
+        const bool hit = r == 1;
+        L.ar += hit ? col.x : 0.0f;
+        L.ag += hit ? col.y : 0.0f;
+        L.ab += hit ? col.z : 0.0f;
+        L.n_s += hit ? 1u : 0u; // arithmetic, not a selected counter (that would live in scratch)
+        L.n_m += hit ? 0u : 1u;
         L.s_next++;
         L.live = false;
     }
@@ -825,7 +846,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
 {
     __shared__ int stack_mem[STACK * 256];
     extern __shared__ float4 lds_scene[];
-    int* stk = stack_mem + threadIdx.x;
+    const TravStack stk{stack_mem + threadIdx.x, p.stack_ovf + blockIdx.x * 256 + threadIdx.x, (int)gridDim.x * 256};
     const ShadeRecs R = stage_scene<LDS>(s, prims_g, mats_g, xf, lds_scene);
     const int lane = threadIdx.x & 63;
     const unsigned total = (unsigned)p.n_chunks * (unsigned)p.n_pad;
@@ -839,7 +860,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
     // traversal state of the lane's current query
     bool trav = false, done = false;
     int ref = 0, sp = 0, k = 0, kend = 0; // [k, kend): primitives of the leaf being tested
-    V3 id{0, 0, 0}, oi{0, 0, 0};
+    V3 id{0, 0, 0}; // 1/d of the query (o/d is recomputed per visit: fewer live registers)
     Best b{__builtin_huge_valf(), -1, 0.0f, 0.0f};
 
     while (true) {
@@ -855,7 +876,6 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
             refill(L, S, p, s, cam, lane, total);
             if (L.live && !trav) { // start the next query
                 id = v3(slab_rcp(S.d.x), slab_rcp(S.d.y), slab_rcp(S.d.z));
-                oi = S.o * id;
                 ref = s.root;
                 sp = 0;
                 k = kend = 0;
@@ -891,18 +911,19 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                 k += RT_LEAF_STEP;
                 pop = k >= kend;
             } else if (WIDTH == 4) {
-                wide_visit<STACK>(nodes4[ref], id, oi, b.t, ref, sp, stk, pop);
+                wide_visit<STACK>(nodes4[ref], id, S.o * id, b.t, ref, sp, stk, pop);
                 if (STATS) cnt.nodes++;
             } else {
                 const NodeF n = nodes[ref];
                 if (STATS) cnt.nodes++;
                 float tl, tr;
+                const V3 oi = S.o * id;
                 const bool hl = slab(n.lmin, n.lmax, oi, id, b.t, tl);
                 const bool hr = slab(n.rmin, n.rmax, oi, id, b.t, tr);
                 const int cl = __float_as_int(n.lmin.w), cr = __float_as_int(n.rmin.w);
                 if (hl && hr) {
                     const bool lf = tl <= tr;
-                    if (sp < STACK) stk[(sp++) * 256] = lf ? cr : cl; // host guarantees depth < STACK
+                    push<STACK>(stk, sp, lf ? cr : cl);
                     ref = lf ? cl : cr;
                     pop = false;
                 } else if (hl | hr) {
@@ -912,7 +933,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
             }
             if (pop) {
                 if (sp > 0) {
-                    ref = stk[(--sp) * 256];
+                    ref = pop_ref<STACK>(stk, sp);
                 } else {
                     trav = false;
                     done = true;
@@ -1027,7 +1048,7 @@ PathKernel pick_bvh(bool stats)
 }
 
 // variant = kernel * 2 + lds; kernel 0 brute force (flat), 1 brute force (grouped, culled),
-// 2/3 BVH2 (24/48-entry stack), 4/5/6 wide BVH (32/40/64)
+// 2 BVH2 (24-entry LDS stack), 3 wide BVH (32-entry LDS stack); both stacks overflow to global memory
 PathKernel pick(int variant, bool stats)
 {
     switch (variant) {
@@ -1036,14 +1057,8 @@ PathKernel pick(int variant, bool stats)
     case 3: return pick_brute<true, true>(stats);
     case 4: return pick_bvh<2, 24, false>(stats);
     case 5: return pick_bvh<2, 24, true>(stats);
-    case 6: return pick_bvh<2, 48, false>(stats);
-    case 7: return pick_bvh<2, 48, true>(stats);
-    case 8: return pick_bvh<4, 32, false>(stats);
-    case 9: return pick_bvh<4, 32, true>(stats);
-    case 10: return pick_bvh<4, 40, false>(stats);
-    case 11: return pick_bvh<4, 40, true>(stats);
-    case 12: return pick_bvh<4, 64, false>(stats);
-    case 13: return pick_bvh<4, 64, true>(stats);
+    case 6: return pick_bvh<4, 32, false>(stats);
+    case 7: return pick_bvh<4, 32, true>(stats);
     default: return pick_brute<false, false>(stats);
     }
 }
@@ -1096,7 +1111,7 @@ hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& 
 {
     PathScene ps = make_path_scene(s);
     const int kernel = variant >> 1;
-    if (kernel >= 4) ps.root = s.root4; // the wide kernels walk the collapsed tree
+    if (kernel == 3) ps.root = s.root4; // the wide kernel walks the collapsed tree
     const bool grouped = kernel == 1, bvh = kernel >= 2;
     ps.n_groups = grouped ? s.n_groups_gr : 1;
     CameraF ca = cam;

@@ -24,6 +24,7 @@ struct PathParams {
     unsigned int* counter;      // work-item dispenser (zeroed before launch), handed out 64 at a time
     float4* partial;            // [block][chunk][64 pixels]: rgb sums, (samples | misses << 16)
     unsigned long long* rays;   // Scene.RayTrace-equivalents (added to)
+    int* stack_ovf;             // BVH kernels: traversal-stack overflow, RT_STACK_OVF entries per lane of the grid
     unsigned long long* stats;  // optional [7]: node visits, triangle tests, sphere tests (per lane);
                                 //   wave cycles in sample start, traversal, shading; wave iterations
 };
@@ -32,10 +33,11 @@ struct PathParams {
 hipError_t launch_primary_ids(const DevScene& s, const CameraD& cam, int x0, int y0, int w, int h, int mode,
                               int32_t* d_ids, hipStream_t stream);
 
-// Kernel variant: kernel 0 brute force, 1 grouped brute force, 2/3 BVH2 (24/48-entry stack),
-// 4/5/6 wide BVH (32/40/64);
+// Kernel variant: kernel 0 brute force, 1 grouped brute force, 2 BVH2 (24-entry stack), 3 wide BVH
+// (32-entry stack), both + kStackOverflow entries in global memory;
 // lds stages the shading records in LDS.
 int path_variant(int kernel, bool lds);
+constexpr int kStackOverflow = 40; // = RT_STACK_OVF (kernels_path.hip)
 size_t path_lds_bytes(const DevScene& s);   // dynamic LDS of the staged (lds) variants
 // Launch the persistent kernel; stats counts node visits / primitive tests (slower build).
 hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& p, int variant, int grid_blocks,

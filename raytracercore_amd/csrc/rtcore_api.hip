@@ -113,6 +113,7 @@ struct rt_scene {
     DevBuf<RefNode> ref_nodes;
     // work buffers
     DevBuf<unsigned int> counter;
+    DevBuf<int> stack_ovf;
     DevBuf<unsigned long long> rays;
     DevBuf<float4> partial;
     DevBuf<double> sum, colors;
@@ -505,21 +506,21 @@ int resolve_traversal(rt_scene* s)
     if (s->traversal == RT_TRAVERSAL_AUTO && t == RT_TRAVERSAL_BRUTE && s->grouped_measured > 1.25)
         t = RT_TRAVERSAL_GROUPED;
     if (t == RT_TRAVERSAL_GROUPED && s->dev.n_groups_gr == 0) t = RT_TRAVERSAL_BRUTE; // too big to group
-    // kernel: 0 brute force, 1 grouped brute force, 2/3 BVH2 with a 24/48-entry stack,
-    // 4/5/6 wide BVH with 32/40/64
+    // kernel: 0 brute force, 1 grouped brute force, 2 BVH2 (24 + kStackOverflow stack entries),
+    // 3 wide BVH (32 + kStackOverflow)
     int kernel = t == RT_TRAVERSAL_GROUPED ? 1 : 0;
     if (t == RT_TRAVERSAL_BVH2) {
-        if (s->sah.depth >= 48) {
-            set_error("BVH2 deeper than the kernel's LDS stack");
+        if (s->sah.depth >= 24 + kStackOverflow) {
+            set_error("BVH2 deeper than the kernel's traversal stack");
             return RT_ERR_ARG;
         }
-        kernel = s->sah.depth < 24 ? 2 : 3;
+        kernel = 2;
     } else if (t == RT_TRAVERSAL_BVH) {
-        if (s->bvh4.stack_need > 64) {
-            set_error("wide BVH needs a deeper traversal stack than the kernel's 64 entries");
+        if (s->bvh4.stack_need > 32 + kStackOverflow) {
+            set_error("wide BVH needs a deeper traversal stack than the kernel's");
             return RT_ERR_ARG;
         }
-        kernel = s->bvh4.stack_need <= 32 ? 4 : s->bvh4.stack_need <= 40 ? 5 : 6;
+        kernel = 3;
     }
     s->resolved = t;
     // Stage the shading records in LDS when that costs no occupancy (RTCORE_PATH_LDS=0/1 forces
@@ -648,6 +649,11 @@ int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t
     p.stats = s->stats_on ? s->stats_buf.p : nullptr;
     HIP_TRY(hipMemsetAsync(p.counter, 0, sizeof(unsigned int), stream));
     const int grid = s->n_cu * (s->stats_on ? s->stats_blocks_per_cu : s->blocks_per_cu);
+    p.stack_ovf = nullptr;
+    if (s->variant >= 4) { // BVH kernels: the stacks' global overflow area
+        HIP_TRY(s->stack_ovf.reserve((size_t)grid * 256 * kStackOverflow));
+        p.stack_ovf = s->stack_ovf.p;
+    }
     HIP_TRY(hipEventRecord(s->ev0, stream));
     HIP_TRY(launch_path(s->dev, s->camf, p, s->variant, grid, stream, s->stats_on));
     HIP_TRY(hipEventRecord(s->ev1, stream));
