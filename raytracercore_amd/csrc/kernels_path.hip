@@ -595,11 +595,14 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
 #ifndef RT_PATH_WAVES
 #define RT_PATH_WAVES 6 // minimum waves per SIMD the register allocator must allow (brute force)
 #endif
+#ifndef RT_WIDE_STACK
+#define RT_WIDE_STACK 40 // LDS entries of the wide BVH kernel's traversal stack (then global overflow)
+#endif
 #ifndef RT_LEAF_STEP
 #define RT_LEAF_STEP 2 // leaf primitives tested per BVH traversal step
 #endif
 #ifndef RT_BVH_WAVES
-#define RT_BVH_WAVES 5 // the same for the BVH kernel (its LDS stack caps occupancy anyway)
+#define RT_BVH_WAVES 4 // the same for the BVH kernel (the wide kernel's 40 KB LDS stack caps it at 4)
 #endif
 
 // LDS staging of the shading records (PrimF per slot, MatF per ID, XformF): the per-lane gathers
@@ -860,7 +863,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
     // traversal state of the lane's current query
     bool trav = false, done = false;
     int ref = 0, sp = 0, k = 0, kend = 0; // [k, kend): primitives of the leaf being tested
-    V3 id{0, 0, 0}; // 1/d of the query (o/d is recomputed per visit: fewer live registers)
+    V3 id{0, 0, 0}, oi{0, 0, 0}; // 1/d and o/d of the query
     Best b{__builtin_huge_valf(), -1, 0.0f, 0.0f};
 
     while (true) {
@@ -876,6 +879,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
             refill(L, S, p, s, cam, lane, total);
             if (L.live && !trav) { // start the next query
                 id = v3(slab_rcp(S.d.x), slab_rcp(S.d.y), slab_rcp(S.d.z));
+                oi = S.o * id;
                 ref = s.root;
                 sp = 0;
                 k = kend = 0;
@@ -911,13 +915,12 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                 k += RT_LEAF_STEP;
                 pop = k >= kend;
             } else if (WIDTH == 4) {
-                wide_visit<STACK>(nodes4[ref], id, S.o * id, b.t, ref, sp, stk, pop);
+                wide_visit<STACK>(nodes4[ref], id, oi, b.t, ref, sp, stk, pop);
                 if (STATS) cnt.nodes++;
             } else {
                 const NodeF n = nodes[ref];
                 if (STATS) cnt.nodes++;
                 float tl, tr;
-                const V3 oi = S.o * id;
                 const bool hl = slab(n.lmin, n.lmax, oi, id, b.t, tl);
                 const bool hr = slab(n.rmin, n.rmax, oi, id, b.t, tr);
                 const int cl = __float_as_int(n.lmin.w), cr = __float_as_int(n.rmin.w);
@@ -1048,7 +1051,7 @@ PathKernel pick_bvh(bool stats)
 }
 
 // variant = kernel * 2 + lds; kernel 0 brute force (flat), 1 brute force (grouped, culled),
-// 2 BVH2 (24-entry LDS stack), 3 wide BVH (32-entry LDS stack); both stacks overflow to global memory
+// 2 BVH2 (24-entry LDS stack), 3 wide BVH (40-entry LDS stack); both stacks overflow to global memory
 PathKernel pick(int variant, bool stats)
 {
     switch (variant) {
@@ -1057,8 +1060,8 @@ PathKernel pick(int variant, bool stats)
     case 3: return pick_brute<true, true>(stats);
     case 4: return pick_bvh<2, 24, false>(stats);
     case 5: return pick_bvh<2, 24, true>(stats);
-    case 6: return pick_bvh<4, 32, false>(stats);
-    case 7: return pick_bvh<4, 32, true>(stats);
+    case 6: return pick_bvh<4, RT_WIDE_STACK, false>(stats);
+    case 7: return pick_bvh<4, RT_WIDE_STACK, true>(stats);
     default: return pick_brute<false, false>(stats);
     }
 }
@@ -1087,6 +1090,8 @@ PathScene make_path_scene(const DevScene& s)
 }
 
 } // namespace
+
+int path_wide_stack() { return RT_WIDE_STACK; }
 
 size_t path_lds_bytes(const DevScene& s)
 {

@@ -34,10 +34,11 @@ hipError_t launch_primary_ids(const DevScene& s, const CameraD& cam, int x0, int
                               int32_t* d_ids, hipStream_t stream);
 
 // Kernel variant: kernel 0 brute force, 1 grouped brute force, 2 BVH2 (24-entry stack), 3 wide BVH
-// (32-entry stack), both + kStackOverflow entries in global memory;
+// (RT_WIDE_STACK = 40-entry stack), both + kStackOverflow entries in global memory;
 // lds stages the shading records in LDS.
 int path_variant(int kernel, bool lds);
 constexpr int kStackOverflow = 40; // = RT_STACK_OVF (kernels_path.hip)
+int path_wide_stack();              // LDS entries of the wide BVH kernel's stack (RT_WIDE_STACK)
 size_t path_lds_bytes(const DevScene& s);   // dynamic LDS of the staged (lds) variants
 // Launch the persistent kernel; stats counts node visits / primitive tests (slower build).
 hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& p, int variant, int grid_blocks,

@@ -507,7 +507,7 @@ int resolve_traversal(rt_scene* s)
         t = RT_TRAVERSAL_GROUPED;
     if (t == RT_TRAVERSAL_GROUPED && s->dev.n_groups_gr == 0) t = RT_TRAVERSAL_BRUTE; // too big to group
     // kernel: 0 brute force, 1 grouped brute force, 2 BVH2 (24 + kStackOverflow stack entries),
-    // 3 wide BVH (32 + kStackOverflow)
+    // 3 wide BVH (RT_WIDE_STACK + kStackOverflow)
     int kernel = t == RT_TRAVERSAL_GROUPED ? 1 : 0;
     if (t == RT_TRAVERSAL_BVH2) {
         if (s->sah.depth >= 24 + kStackOverflow) {
@@ -516,7 +516,7 @@ int resolve_traversal(rt_scene* s)
         }
         kernel = 2;
     } else if (t == RT_TRAVERSAL_BVH) {
-        if (s->bvh4.stack_need > 32 + kStackOverflow) {
+        if (s->bvh4.stack_need > path_wide_stack() + kStackOverflow) {
             set_error("wide BVH needs a deeper traversal stack than the kernel's");
             return RT_ERR_ARG;
         }
