@@ -277,6 +277,8 @@ def main() -> int:
             "roofline": roofline(args.config, fpr, bpr, my_rays_per_step, avg_ms),
             "path_stats": {"per_ray": {k: round(st[k], 3) for k in ("nodes", "tris", "sphs")},
                            "lane_slots_per_ray": st["wave_iters_per_ray"]},
+            "scene_build": {"builder": ["auto", "host", "gpu"][info.bvh_builder],
+                            **{k: round(v, 2) for k, v in gpu.build_stats().items()}},
         }
         traffic_file = os.path.join(ROOT, "profiles", "traffic", f"{args.config}.json")
         if os.path.exists(traffic_file) and args.spp == 0:  # PMC bytes of this launch shape (tools/profile.sh)

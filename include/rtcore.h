@@ -142,9 +142,23 @@ typedef struct rt_scene_info {
     int32_t sah_bvh_depth;
     int32_t traversal;       /* resolved rt_traversal of the path kernel                  */
     int32_t device;
-    int32_t reserved;
+    int32_t bvh_builder;     /* rt_bvh_builder that built the kernel's BVHs               */
     uint64_t device_bytes;   /* scene bytes resident in HBM                               */
 } rt_scene_info;
+
+/* Who builds the path kernel's BVH2 and its wide collapse at rt_scene_create. */
+typedef enum rt_bvh_builder {
+    RT_BVH_BUILDER_AUTO = 0, /* the GPU from 2^22 BVH primitives on, the host below
+                                (RTCORE_BVH_BUILDER=host|gpu overrides AUTO)          */
+    RT_BVH_BUILDER_HOST = 1, /* binned SAH on the host, collapsed to 4-wide            */
+    RT_BVH_BUILDER_GPU = 2   /* PLOC on the device (Morton order, nearest-neighbour
+                                merges by merged-box area), collapsed on the device   */
+} rt_bvh_builder;
+
+/* rt_scene_get_build_stats: [0] host preparation ms, [1] BVH build ms (wall, either
+   builder), [2] upload ms, [3] GPU builder device ms, [4] PLOC rounds, [5] wide nodes,
+   [6] wide-tree stack need */
+#define RT_BUILD_STATS_COUNT 7
 
 /* ---------------------------------------------------------------- library ---- */
 int rt_abi_version(void);
@@ -159,6 +173,14 @@ int rt_scene_set_camera(rt_scene* scene, const rt_camera* camera);
 int rt_scene_set_traversal(rt_scene* scene, int32_t traversal);
 int rt_scene_get_info(const rt_scene* scene, rt_scene_info* info);
 void rt_scene_destroy(rt_scene* scene);
+/* Process-wide builder choice for later rt_scene_create calls (default AUTO). */
+int rt_set_bvh_builder(int32_t builder);
+/* Copies min(n, RT_BUILD_STATS_COUNT) build statistics of the scene (see above). */
+int rt_scene_get_build_stats(const rt_scene* scene, double* out, int32_t n);
+/* Validation: checks the device-resident BVH2 and wide tree against the primitives (every
+   child box contains the primitives below it, each primitive in exactly one leaf, depth and
+   stack within what the kernels were sized for).  RT_ERR_STATE with the finding otherwise. */
+int rt_scene_check_bvh(rt_scene* scene);
 
 /* ------------------------------------------------------- host-buffer renders --- */
 /*

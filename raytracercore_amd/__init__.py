@@ -27,6 +27,8 @@ RT_PRIM_TRIANGLE, RT_PRIM_SPHERE, RT_PRIM_PLANE = 0, 1, 2
 RT_FLAG_MIRROR, RT_FLAG_TWOSIDED, RT_FLAG_INVERT, RT_FLAG_HASNORMALS, RT_FLAG_TRANSFORMED = 1, 2, 4, 8, 16
 RT_CAMERA_FRUSTUM, RT_CAMERA_ORTHO = 0, 1
 RT_TRAVERSAL_AUTO, RT_TRAVERSAL_BRUTE, RT_TRAVERSAL_BVH, RT_TRAVERSAL_BVH2, RT_TRAVERSAL_GROUPED = 0, 1, 2, 3, 4
+RT_BVH_BUILDER_AUTO, RT_BVH_BUILDER_HOST, RT_BVH_BUILDER_GPU = 0, 1, 2
+BUILD_STAT_NAMES = ("prepare_ms", "bvh_ms", "upload_ms", "gpu_build_ms", "ploc_rounds", "wide_nodes", "stack_need")
 
 
 class RtError(RuntimeError):
@@ -72,7 +74,7 @@ class rt_scene_info(C.Structure):
     _fields_ = [
         ("n_prims", C.c_int32), ("ref_bvh_nodes", C.c_int32), ("ref_bvh_depth", C.c_int32),
         ("sah_bvh_nodes", C.c_int32), ("sah_bvh_depth", C.c_int32), ("traversal", C.c_int32),
-        ("device", C.c_int32), ("reserved", C.c_int32), ("device_bytes", C.c_uint64),
+        ("device", C.c_int32), ("bvh_builder", C.c_int32), ("device_bytes", C.c_uint64),
     ]
 
 
@@ -107,6 +109,9 @@ def load_library(path: str = "") -> C.CDLL:
         "rt_scene_set_traversal": (C.c_int, [C.c_void_p, C.c_int32]),
         "rt_scene_get_info": (C.c_int, [C.c_void_p, P(rt_scene_info)]),
         "rt_scene_destroy": (None, [C.c_void_p]),
+        "rt_set_bvh_builder": (C.c_int, [C.c_int32]),
+        "rt_scene_get_build_stats": (C.c_int, [C.c_void_p, P(C.c_double), C.c_int32]),
+        "rt_scene_check_bvh": (C.c_int, [C.c_void_p]),
         "rt_render_tile": (C.c_int, [C.c_void_p] + [C.c_int32] * 5 + [C.c_uint64, C.c_uint64,
                                      P(rt_color), P(C.c_uint32), P(C.c_uint32), P(C.c_uint64)]),
         "rt_render_tile_1spp": (C.c_int, [C.c_void_p] + [C.c_int32] * 4 + [C.c_uint64, C.c_uint64, P(rt_color)]),
@@ -207,7 +212,8 @@ class GpuRaytracer:
     """
 
     def __init__(self, scene: ParsedScene, camera_index: int = 0, device: int = 0,
-                 size: Optional[Tuple[int, int]] = None, traversal: int = RT_TRAVERSAL_AUTO):
+                 size: Optional[Tuple[int, int]] = None, traversal: int = RT_TRAVERSAL_AUTO,
+                 builder: Optional[int] = None):
         lib = load_library()
         self.lib = lib
         self.params = rt_scene_params.from_buffer_copy(scene.params)
@@ -216,8 +222,14 @@ class GpuRaytracer:
         self.width, self.height = self.params.width, self.params.height
         self.handle = C.c_void_p()
         n = scene.n_prims
-        prims = (rt_prim * max(1, n))(*scene.prims)
-        _check(lib.rt_scene_create(C.byref(self.params), prims, n, device, C.byref(self.handle)))
+        prims = scene.prims if isinstance(scene.prims, C.Array) and n > 0 else (rt_prim * max(1, n))(*scene.prims)
+        if builder is not None:  # process-wide in the library: set for this create only
+            _check(lib.rt_set_bvh_builder(builder))
+        try:
+            _check(lib.rt_scene_create(C.byref(self.params), prims, n, device, C.byref(self.handle)))
+        finally:
+            if builder is not None:
+                lib.rt_set_bvh_builder(RT_BVH_BUILDER_AUTO)
         self.device = device
         if len(scene.cameras) == 0:
             raise RtError("scene has no camera")
@@ -244,6 +256,16 @@ class GpuRaytracer:
         inf = rt_scene_info()
         _check(self.lib.rt_scene_get_info(self.handle, C.byref(inf)))
         return inf
+
+    def check_bvh(self) -> None:
+        """rt_scene_check_bvh: structural validation of the device BVHs (raises RtError)."""
+        _check(self.lib.rt_scene_check_bvh(self.handle))
+
+    def build_stats(self) -> dict:
+        """rt_scene_get_build_stats: scene-creation timings and the BVH builder's figures."""
+        out = (C.c_double * len(BUILD_STAT_NAMES))()
+        _check(self.lib.rt_scene_get_build_stats(self.handle, out, len(BUILD_STAT_NAMES)))
+        return dict(zip(BUILD_STAT_NAMES, (float(v) for v in out)))
 
     def primary_ids(self, x0: int = 0, y0: int = 0, w: Optional[int] = None, h: Optional[int] = None) -> np.ndarray:
         """DebugRaycaster Primitives-mode IDs as an int32 array indexed [x, y]."""

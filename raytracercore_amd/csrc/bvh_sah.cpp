@@ -167,6 +167,17 @@ int leaf_ref(int first, int count) { return ~((first << 3) | (count - 1)); }
 
 } // namespace
 
+void sah_prim_box(const HostPrim& p, float lo[3], float hi[3])
+{
+    const double l[3] = {p.box.mn.x, p.box.mn.y, p.box.mn.z}, h[3] = {p.box.mx.x, p.box.mx.y, p.box.mx.z};
+    for (int k = 0; k < 3; k++) {
+        // outward rounding plus a relative pad of 2^-20 against fp32 traversal rounding
+        const double pad = (std::fabs(l[k]) + std::fabs(h[k])) * 9.5367431640625e-07 + 1e-30;
+        lo[k] = round_down(l[k] - pad);
+        hi[k] = round_up(h[k] + pad);
+    }
+}
+
 SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf)
 {
     SahBvh out;
@@ -177,14 +188,8 @@ SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf)
         if (p.kind == RT_PRIM_PLANE) continue;
         Ref r;
         r.prim = i;
-        const double lo[3] = {p.box.mn.x, p.box.mn.y, p.box.mn.z}, hi[3] = {p.box.mx.x, p.box.mx.y, p.box.mx.z};
-        for (int k = 0; k < 3; k++) {
-            // outward rounding plus a relative pad of 2^-20 against fp32 traversal rounding
-            double pad = (std::fabs(lo[k]) + std::fabs(hi[k])) * 9.5367431640625e-07 + 1e-30;
-            r.box.lo[k] = round_down(lo[k] - pad);
-            r.box.hi[k] = round_up(hi[k] + pad);
-            r.c[k] = 0.5f * (r.box.lo[k] + r.box.hi[k]);
-        }
+        sah_prim_box(p, r.box.lo, r.box.hi);
+        for (int k = 0; k < 3; k++) r.c[k] = 0.5f * (r.box.lo[k] + r.box.hi[k]);
         b.refs.push_back(r);
     }
     if (b.refs.empty()) {
@@ -295,54 +300,13 @@ struct W4Builder {
         int refs[4] = {RT_NODE4_EMPTY, RT_NODE4_EMPTY, RT_NODE4_EMPTY, RT_NODE4_EMPTY};
         for (int k = 0; k < nc; k++)
             refs[k] = ch[k].ref >= 0 ? emit(ch[k].ref, level + 1, pushes + nc - 1) : ch[k].ref;
-        // quantisation frame
-        FBox nb;
-        nb.empty();
-        for (const WChild& c : ch) nb.grow(c.box);
-        float org[3];
-        int ex[3];
-        uint32_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
-        for (int a = 0; a < 3; a++) {
-            org[a] = nb.lo[a];
-            const double ext = (double)nb.hi[a] - (double)nb.lo[a];
-            int e = ext > 0 ? (int)std::ceil(std::log2(ext / 255.0)) : -100;
-            e = std::max(e, -100);
-            while ((double)(float)((double)org[a] + 255.0 * std::ldexp(1.0, e)) < (double)nb.hi[a]) e++;
-            ex[a] = e;
-            const double sc = std::ldexp(1.0, e);
-            for (int k = 0; k < 4; k++) {
-                uint32_t lo8 = 255, hi8 = 0; // empty slot: inverted box
-                if (k < nc) {
-                    double ql = std::floor(((double)ch[k].box.lo[a] - (double)org[a]) / sc);
-                    double qh = std::ceil(((double)ch[k].box.hi[a] - (double)org[a]) / sc);
-                    ql = std::min(255.0, std::max(0.0, ql));
-                    qh = std::min(255.0, std::max(0.0, qh));
-                    // the fp32 dequantised planes must contain the child box
-                    while (ql > 0 && (float)((double)org[a] + ql * sc) > ch[k].box.lo[a]) ql -= 1;
-                    while (qh < 255 && (float)((double)org[a] + qh * sc) < ch[k].box.hi[a]) qh += 1;
-                    lo8 = (uint32_t)ql;
-                    hi8 = (uint32_t)qh;
-                }
-                qlo[a] |= lo8 << (8 * k);
-                qhi[a] |= hi8 << (8 * k);
+        float lo[4][3], hi[4][3];
+        for (int k = 0; k < nc; k++)
+            for (int a = 0; a < 3; a++) {
+                lo[k][a] = ch[k].box.lo[a];
+                hi[k][a] = ch[k].box.hi[a];
             }
-        }
-        Node4Q q;
-        uint32_t exps = (uint32_t)(ex[0] + 128) | ((uint32_t)(ex[1] + 128) << 8) | ((uint32_t)(ex[2] + 128) << 16);
-        auto f = [](uint32_t u) {
-            float v;
-            std::memcpy(&v, &u, 4);
-            return v;
-        };
-        auto fi = [](int u) {
-            float v;
-            std::memcpy(&v, &u, 4);
-            return v;
-        };
-        q.a = make_float4(org[0], org[1], org[2], f(exps));
-        q.b = make_float4(f(qlo[0]), f(qhi[0]), f(qlo[1]), f(qhi[1]));
-        q.c = make_float4(f(qlo[2]), f(qhi[2]), fi(refs[0]), fi(refs[1]));
-        q.d = make_float4(fi(refs[2]), fi(refs[3]), fi(nc), 0.0f);
+        const Node4Q q = quantize_node4(lo, hi, refs, nc);
         out[me] = q;
         return me;
     }

@@ -1,11 +1,34 @@
 // host_scene.h -- host-side preparation of a scene for the MI355X kernels.
 #pragma once
+#include <algorithm>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rt_refmath.h"
 
 namespace rtc {
+
+// fn(i) for i in [0, n) on up to 16 host threads (at least 4096 items each); fn must only
+// write state of its own index.
+template <class F>
+void parallel_for(int n, F&& fn)
+{
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    const int T = std::min(std::min(hw, 16), (n + 4095) / 4096);
+    if (T <= 1) {
+        for (int i = 0; i < n; i++) fn(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    const int per = (n + T - 1) / T;
+    for (int t = 0; t < T; t++)
+        th.emplace_back([&fn, t, per, n] {
+            const int a = t * per, b = std::min(n, a + per);
+            for (int i = a; i < b; i++) fn(i);
+        });
+    for (auto& x : th) x.join();
+}
 
 // Axis-aligned box in the reference's fp64 representation (Acceleration/AABB.cs:44-64).
 struct Box {
@@ -54,6 +77,9 @@ struct SahBvh {
     int depth = 0;
 };
 SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf);
+// fp32 box of a primitive for the fast-path BVHs: the fp64 bounds padded by 2^-20 relative and
+// rounded outward (used by the host and the GPU builder alike)
+void sah_prim_box(const HostPrim& p, float lo[3], float hi[3]);
 
 struct Bvh4 {
     std::vector<Node4Q> nodes;

@@ -153,6 +153,64 @@ struct alignas(16) Node4Q {
     float4 a, b, c, d;
 };
 
+__host__ __device__ inline float bits_f(uint32_t u)
+{
+    float f;
+    __builtin_memcpy(&f, &u, 4);
+    return f;
+}
+
+// Quantise up to four child boxes (fp32, lo/hi per axis) into a Node4Q.  Shared by the host
+// collapse (bvh_sah.cpp) and the GPU builder (bvh_gpu.hip), in fp64: the exponent is the smallest
+// e with origin + 255 * 2^e >= the node's upper plane in fp32, and each child plane is rounded
+// outward until its fp32 dequantised value contains the child box.
+__host__ __device__ inline Node4Q quantize_node4(const float lo[4][3], const float hi[4][3], const int refs_in[4],
+                                                 int nc)
+{
+    float org[3];
+    int ex[3];
+    uint32_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
+    for (int a = 0; a < 3; a++) {
+        float nlo = __builtin_huge_valf(), nhi = -__builtin_huge_valf();
+        for (int k = 0; k < nc; k++) {
+            nlo = lo[k][a] < nlo ? lo[k][a] : nlo;
+            nhi = hi[k][a] > nhi ? hi[k][a] : nhi;
+        }
+        org[a] = nlo;
+        const double ext = (double)nhi - (double)nlo;
+        int e = ext > 0 ? (int)ceil(log2(ext / 255.0)) : -100;
+        e = e > -100 ? e : -100;
+        while ((double)(float)((double)org[a] + 255.0 * ldexp(1.0, e)) < (double)nhi) e++;
+        ex[a] = e;
+        const double sc = ldexp(1.0, e);
+        for (int k = 0; k < 4; k++) {
+            uint32_t lo8 = 255, hi8 = 0; // empty slot: inverted box
+            if (k < nc) {
+                double ql = floor(((double)lo[k][a] - (double)org[a]) / sc);
+                double qh = ceil(((double)hi[k][a] - (double)org[a]) / sc);
+                ql = ql < 0.0 ? 0.0 : (ql > 255.0 ? 255.0 : ql);
+                qh = qh < 0.0 ? 0.0 : (qh > 255.0 ? 255.0 : qh);
+                // the fp32 dequantised planes must contain the child box
+                while (ql > 0 && (float)((double)org[a] + ql * sc) > lo[k][a]) ql -= 1;
+                while (qh < 255 && (float)((double)org[a] + qh * sc) < hi[k][a]) qh += 1;
+                lo8 = (uint32_t)ql;
+                hi8 = (uint32_t)qh;
+            }
+            qlo[a] |= lo8 << (8 * k);
+            qhi[a] |= hi8 << (8 * k);
+        }
+    }
+    int refs[4] = {RT_NODE4_EMPTY, RT_NODE4_EMPTY, RT_NODE4_EMPTY, RT_NODE4_EMPTY};
+    for (int k = 0; k < nc; k++) refs[k] = refs_in[k];
+    const uint32_t exps = (uint32_t)(ex[0] + 128) | ((uint32_t)(ex[1] + 128) << 8) | ((uint32_t)(ex[2] + 128) << 16);
+    Node4Q q;
+    q.a = make_float4(org[0], org[1], org[2], bits_f(exps));
+    q.b = make_float4(bits_f(qlo[0]), bits_f(qhi[0]), bits_f(qlo[1]), bits_f(qhi[1]));
+    q.c = make_float4(bits_f(qlo[2]), bits_f(qhi[2]), bits_f((uint32_t)refs[0]), bits_f((uint32_t)refs[1]));
+    q.d = make_float4(bits_f((uint32_t)refs[2]), bits_f((uint32_t)refs[3]), bits_f((uint32_t)nc), 0.0f);
+    return q;
+}
+
 struct CameraF {                // post-InitRender state in fp32 (path kernel)
     float4 position, look, side, up;
     float w2, h2, tan_x, tan_y, h_mult, v_mult, image_plane, dof, focal_length;

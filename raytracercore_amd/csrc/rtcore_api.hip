@@ -6,7 +6,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -15,6 +18,7 @@
 #include <vector>
 
 #include "../../include/rtcore_rng.h"
+#include "bvh_gpu.h"
 #include "host_scene.h"
 #include "rt_kernels.h"
 
@@ -55,6 +59,12 @@ struct DevBuf {
         if (e == hipSuccess) n = count;
         return e;
     }
+    void adopt(T* q, size_t count) // take ownership of a hipMalloc'd array
+    {
+        release();
+        p = q;
+        n = q ? count : 0;
+    }
     hipError_t upload(const std::vector<T>& v)
     {
         hipError_t e = reserve(v.size());
@@ -91,8 +101,15 @@ struct rt_scene {
     int blocks_per_cu = 1;
     RefBvh ref;
     bool ref_built = false;
-    SahBvh sah;
+    SahBvh sah;   // host-built trees (empty when the GPU builder made them)
     Bvh4 bvh4;
+    struct {
+        int builder = RT_BVH_BUILDER_HOST; // the one that ran
+        int n_nodes2 = 0, n_nodes4 = 0, root2 = 0, root4 = 0, depth2 = 0, stack4 = 0, rounds = 0;
+        float gpu_ms = 0.0f;
+    } bvh;
+    DevBuf<int32_t> order_d;      // GPU builder: primitive IDs in leaf order, planes appended
+    double ms_prepare = 0, ms_bvh = 0, ms_upload = 0;
     DevScene dev{};
     DevBuf<PrimF> prims_bf, prims_bvh;
     DevBuf<TestRec> tests_bf, tests_bvh;
@@ -389,15 +406,46 @@ int upload_scene(rt_scene* s)
     BruteOrder grouped = cut.empty() ? BruteOrder{} : build_order(cut);
     std::vector<PrimF> bv;
     std::vector<TestRec> tbv;
-    for (int i : s->sah.order) {
-        bv.push_back(primf(i));
-        tbv.push_back(testrec(i));
-    }
-    for (int i = 0; i < n; i++) // planes follow the BVH's primitives in both orders
-        if (H[i].kind == RT_PRIM_PLANE) {
+    size_t n_bvh_records = 0;
+    if (s->bvh.builder == RT_BVH_BUILDER_GPU) {
+        // records in ID order, gathered on the device into the GPU builder's leaf order
+        std::vector<PrimF> pid(n);
+        std::vector<TestRec> tid(n);
+        parallel_for(n, [&](int i) {
+            pid[i] = primf(i);
+            tid[i] = testrec(i);
+        });
+        std::vector<int32_t> planes;
+        for (int i = 0; i < n; i++)
+            if (H[i].kind == RT_PRIM_PLANE) planes.push_back(i); // planes follow the BVH's primitives
+        const int nb = s->order_d.n > 0 ? (int)s->order_d.n - (int)planes.size() - 1 : 0;
+        n_bvh_records = (size_t)nb + planes.size();
+        if (!planes.empty())
+            HIP_TRY(hipMemcpy(s->order_d.p + nb, planes.data(), planes.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+        DevBuf<PrimF> pid_d;
+        DevBuf<TestRec> tid_d;
+        HIP_TRY(pid_d.upload(pid));
+        HIP_TRY(tid_d.upload(tid));
+        HIP_TRY(s->prims_bvh.reserve(n_bvh_records));
+        HIP_TRY(s->tests_bvh.reserve(n_bvh_records + 1));
+        HIP_TRY(gather_bvh_records(s->order_d.p, (int)n_bvh_records, pid_d.p, tid_d.p, s->prims_bvh.p, s->tests_bvh.p,
+                                   s->stream));
+        // spare record: the BVH leaf step loads one past a leaf
+        HIP_TRY(hipMemsetAsync(s->tests_bvh.p + n_bvh_records, 0, sizeof(TestRec), s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        s->order_d.release();
+    } else {
+        for (int i : s->sah.order) {
             bv.push_back(primf(i));
             tbv.push_back(testrec(i));
         }
+        for (int i = 0; i < n; i++) // planes follow the BVH's primitives in both orders
+            if (H[i].kind == RT_PRIM_PLANE) {
+                bv.push_back(primf(i));
+                tbv.push_back(testrec(i));
+            }
+        n_bvh_records = bv.size();
+    }
     std::vector<MatF> mats(n);
     for (int i = 0; i < n; i++) {
         const HostPrim& p = H[i];
@@ -424,19 +472,20 @@ int upload_scene(rt_scene* s)
     HIP_TRY(s->tests_gr.upload(grouped.tests));
     HIP_TRY(s->rects_gr.upload(grouped.rects));
     HIP_TRY(s->groups_gr.upload(grouped.groups));
-    HIP_TRY(s->prims_bvh.upload(bv));
-    tbv.push_back(TestRec{}); // spare record: the BVH leaf step loads one past a leaf
-    HIP_TRY(s->tests_bvh.upload(tbv));
-    HIP_TRY(s->nodes.upload(s->sah.nodes));
-    HIP_TRY(s->nodes4.upload(s->bvh4.nodes));
+    if (s->bvh.builder != RT_BVH_BUILDER_GPU) {
+        HIP_TRY(s->prims_bvh.upload(bv));
+        tbv.push_back(TestRec{}); // spare record: the BVH leaf step loads one past a leaf
+        HIP_TRY(s->tests_bvh.upload(tbv));
+        HIP_TRY(s->nodes.upload(s->sah.nodes));
+        HIP_TRY(s->nodes4.upload(s->bvh4.nodes));
+    }
     HIP_TRY(s->xf.upload(xf));
     HIP_TRY(s->mats.upload(mats));
     HIP_TRY(s->vnormals.upload(vn));
     s->device_bytes = pd.size() * sizeof(PrimD) + xd.size() * sizeof(XformD) +
-                      (flat.prims.size() + grouped.prims.size() + bv.size()) * sizeof(PrimF) +
-                      (flat.tests.size() + grouped.tests.size() + tbv.size()) * sizeof(TestRec) +
-                      s->sah.nodes.size() * sizeof(NodeF) +
-                      s->bvh4.nodes.size() * sizeof(Node4Q) +
+                      (flat.prims.size() + grouped.prims.size() + n_bvh_records) * sizeof(PrimF) +
+                      (flat.tests.size() + grouped.tests.size() + n_bvh_records + 1) * sizeof(TestRec) +
+                      (size_t)s->bvh.n_nodes2 * sizeof(NodeF) + (size_t)s->bvh.n_nodes4 * sizeof(Node4Q) +
                       xf.size() * sizeof(XformF) + mats.size() * sizeof(MatF) + vn.size() * sizeof(float4);
 
     DevScene& d = s->dev;
@@ -456,11 +505,11 @@ int upload_scene(rt_scene* s)
     d.n_pln = np;
     d.prims_bvh = s->prims_bvh.p;
     d.nodes = s->nodes.p;
-    d.n_nodes = (int)s->sah.nodes.size();
-    d.root = s->sah.root;
+    d.n_nodes = s->bvh.n_nodes2;
+    d.root = s->bvh.root2;
     d.nodes4 = s->nodes4.p;
-    d.n_nodes4 = (int)s->bvh4.nodes.size();
-    d.root4 = s->bvh4.root;
+    d.n_nodes4 = s->bvh.n_nodes4;
+    d.root4 = s->bvh.root4;
     d.xf = s->xf.p;
     d.mats = s->mats.p;
     d.vnormals = s->vnormals.p;
@@ -510,13 +559,13 @@ int resolve_traversal(rt_scene* s)
     // 3 wide BVH (RT_WIDE_STACK + kStackOverflow)
     int kernel = t == RT_TRAVERSAL_GROUPED ? 1 : 0;
     if (t == RT_TRAVERSAL_BVH2) {
-        if (s->sah.depth >= 24 + kStackOverflow) {
+        if (s->bvh.depth2 >= 24 + kStackOverflow) {
             set_error("BVH2 deeper than the kernel's traversal stack");
             return RT_ERR_ARG;
         }
         kernel = 2;
     } else if (t == RT_TRAVERSAL_BVH) {
-        if (s->bvh4.stack_need > path_wide_stack() + kStackOverflow) {
+        if (s->bvh.stack4 > path_wide_stack() + kStackOverflow) {
             set_error("wide BVH needs a deeper traversal stack than the kernel's");
             return RT_ERR_ARG;
         }
@@ -664,6 +713,257 @@ int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t
 
 extern "C" {
 
+namespace {
+std::atomic<int> g_builder{RT_BVH_BUILDER_AUTO};
+// AUTO builds on the GPU from this many BVH primitives.  Below it the host's binned-SAH tree is
+// worth its build time: on the 1 M-triangle mesh (C4) the PLOC tree costs 15 % more node visits
+// and 8 % of the render rate, against 0.4 s of build time saved.
+constexpr int kGpuBuildMin = 1 << 22;
+
+int builder_for(int n_bvh)
+{
+    int b = g_builder.load();
+    if (b == RT_BVH_BUILDER_AUTO)
+        if (const char* e = getenv("RTCORE_BVH_BUILDER")) // for A/B measurements
+            b = std::strcmp(e, "gpu") == 0 ? RT_BVH_BUILDER_GPU : std::strcmp(e, "host") == 0 ? RT_BVH_BUILDER_HOST : b;
+    if (b == RT_BVH_BUILDER_AUTO) b = n_bvh >= kGpuBuildMin ? RT_BVH_BUILDER_GPU : RT_BVH_BUILDER_HOST;
+    return n_bvh > 0 ? b : RT_BVH_BUILDER_HOST;
+}
+
+// The fast-path BVH2 and its wide collapse, by the host (binned SAH, bvh_sah.cpp) or the GPU
+// (PLOC, bvh_gpu.hip).  Planes are never in the BVH.
+int build_bvhs(rt_scene* s)
+{
+    const auto& H = s->host;
+    const int n = (int)H.size();
+    std::vector<int32_t> ids;
+    for (int i = 0; i < n; i++)
+        if (H[i].kind != RT_PRIM_PLANE) ids.push_back(i);
+    const int nb = (int)ids.size();
+    const int max_leaf = n > 256 ? 4 : 2;
+    s->bvh.builder = builder_for(nb);
+    if (s->bvh.builder == RT_BVH_BUILDER_HOST) {
+        s->sah = build_sah_bvh(H, max_leaf);
+        s->bvh4 = build_bvh4(s->sah);
+        s->bvh.n_nodes2 = (int)s->sah.nodes.size();
+        s->bvh.root2 = s->sah.root;
+        s->bvh.depth2 = s->sah.depth;
+        s->bvh.n_nodes4 = (int)s->bvh4.nodes.size();
+        s->bvh.root4 = s->bvh4.root;
+        s->bvh.stack4 = s->bvh4.stack_need;
+        return RT_OK;
+    }
+    std::vector<float4> lo(nb), hi(nb);
+    parallel_for(nb, [&](int k) {
+        float l[3], h[3];
+        sah_prim_box(H[ids[k]], l, h);
+        lo[k] = make_float4(l[0], l[1], l[2], 0.0f);
+        hi[k] = make_float4(h[0], h[1], h[2], 0.0f);
+    });
+    int n_planes = n - nb;
+    GpuBvh g;
+    HIP_TRY(build_bvh_gpu(lo.data(), hi.data(), ids.data(), nb, max_leaf, n_planes + 1, s->stream, g));
+    s->nodes.adopt(g.nodes, g.n_nodes);
+    s->nodes4.adopt(g.nodes4, g.n_nodes4);
+    s->order_d.adopt(g.order, (size_t)nb + n_planes + 1);
+    s->bvh.n_nodes2 = g.n_nodes;
+    s->bvh.root2 = g.root;
+    s->bvh.depth2 = g.depth;
+    s->bvh.n_nodes4 = g.n_nodes4;
+    s->bvh.root4 = g.root4;
+    s->bvh.stack4 = g.stack_need;
+    s->bvh.rounds = g.rounds;
+    s->bvh.gpu_ms = g.ms;
+    return RT_OK;
+}
+} // namespace
+
+int rt_set_bvh_builder(int32_t builder)
+{
+    if (builder < RT_BVH_BUILDER_AUTO || builder > RT_BVH_BUILDER_GPU) {
+        set_error("rt_set_bvh_builder: bad argument");
+        return RT_ERR_ARG;
+    }
+    g_builder.store(builder);
+    return RT_OK;
+}
+
+int rt_scene_get_build_stats(const rt_scene* s, double* out, int32_t n)
+{
+    if (!s || !out || n < 0) {
+        set_error("rt_scene_get_build_stats: bad argument");
+        return RT_ERR_ARG;
+    }
+    const double v[RT_BUILD_STATS_COUNT] = {s->ms_prepare, s->ms_bvh, s->ms_upload, (double)s->bvh.gpu_ms,
+                                           (double)s->bvh.rounds, (double)s->bvh.n_nodes4, (double)s->bvh.stack4};
+    for (int i = 0; i < n && i < RT_BUILD_STATS_COUNT; i++) out[i] = v[i];
+    return RT_OK;
+}
+
+// Structural check of the device-resident fast-path BVHs (either builder): every child box of
+// the BVH2 and every dequantised child box of the wide tree contains the boxes of all primitives
+// below it, every non-plane primitive sits in exactly one leaf of each tree, and the depth and
+// stack figures the kernels were sized by are not exceeded.
+int rt_scene_check_bvh(rt_scene* s)
+{
+    if (!s) {
+        set_error("rt_scene_check_bvh: bad argument");
+        return RT_ERR_ARG;
+    }
+    HIP_TRY(hipSetDevice(s->device));
+    const auto& H = s->host;
+    const int n = (int)H.size();
+    int nb = 0;
+    for (const HostPrim& p : H) nb += p.kind != RT_PRIM_PLANE;
+    std::vector<NodeF> n2(s->bvh.n_nodes2);
+    std::vector<Node4Q> n4(s->bvh.n_nodes4);
+    std::vector<PrimF> recs(nb);
+    if (!n2.empty()) HIP_TRY(hipMemcpy(n2.data(), s->nodes.p, n2.size() * sizeof(NodeF), hipMemcpyDeviceToHost));
+    if (!n4.empty()) HIP_TRY(hipMemcpy(n4.data(), s->nodes4.p, n4.size() * sizeof(Node4Q), hipMemcpyDeviceToHost));
+    if (nb > 0) HIP_TRY(hipMemcpy(recs.data(), s->prims_bvh.p, nb * sizeof(PrimF), hipMemcpyDeviceToHost));
+    std::vector<int> id(nb);
+    for (int k = 0; k < nb; k++) std::memcpy(&id[k], &recs[k].a.w, 4);
+    struct B {
+        double lo[3], hi[3];
+    };
+    auto empty = [] {
+        B b;
+        for (int a = 0; a < 3; a++) {
+            b.lo[a] = __builtin_huge_val();
+            b.hi[a] = -__builtin_huge_val();
+        }
+        return b;
+    };
+    auto grow = [](B& b, const B& c) {
+        for (int a = 0; a < 3; a++) {
+            b.lo[a] = std::min(b.lo[a], c.lo[a]);
+            b.hi[a] = std::max(b.hi[a], c.hi[a]);
+        }
+    };
+    std::vector<B> pbox(n);
+    for (int i = 0; i < n; i++)
+        if (H[i].kind != RT_PRIM_PLANE) {
+            float l[3], h[3];
+            sah_prim_box(H[i], l, h);
+            for (int a = 0; a < 3; a++) {
+                pbox[i].lo[a] = l[a];
+                pbox[i].hi[a] = h[a];
+            }
+        }
+    std::string err;
+    std::vector<int> seen(n, 0);
+    auto leaf = [&](int ref, B& u) {
+        const int code = ~ref, first = code >> 3, cnt = (code & 7) + 1;
+        if (first < 0 || first + cnt > nb) {
+            err = "leaf range out of bounds";
+            return;
+        }
+        for (int k = first; k < first + cnt; k++) {
+            const int p = id[k];
+            if (p < 0 || p >= n || H[p].kind == RT_PRIM_PLANE) {
+                err = "leaf record with a bad primitive ID";
+                return;
+            }
+            seen[p]++;
+            grow(u, pbox[p]);
+        }
+    };
+    auto contains = [](const B& outer, const B& inner) {
+        for (int a = 0; a < 3; a++)
+            if (!(outer.lo[a] <= inner.lo[a] && outer.hi[a] >= inner.hi[a])) return false;
+        return true;
+    };
+    // BVH2
+    int max_depth = 0;
+    std::function<B(int, int)> walk2 = [&](int ref, int depth) -> B {
+        B u = empty();
+        max_depth = std::max(max_depth, depth);
+        if (!err.empty()) return u;
+        if (ref < 0) {
+            leaf(ref, u);
+            return u;
+        }
+        if (ref >= (int)n2.size()) {
+            err = "BVH2 child index out of range";
+            return u;
+        }
+        const NodeF& q = n2[ref];
+        for (int side = 0; side < 2; side++) {
+            const float4 lo = side ? q.rmin : q.lmin, hi = side ? q.rmax : q.lmax;
+            int c;
+            std::memcpy(&c, &lo.w, 4);
+            const B sub = walk2(c, depth + 1);
+            const B box{{lo.x, lo.y, lo.z}, {hi.x, hi.y, hi.z}};
+            if (err.empty() && !contains(box, sub)) err = "BVH2 child box misses a primitive below it";
+            grow(u, sub);
+        }
+        return u;
+    };
+    if (nb > 0) walk2(s->bvh.root2, 0);
+    for (int i = 0; i < n && err.empty(); i++)
+        if (seen[i] != (H[i].kind == RT_PRIM_PLANE ? 0 : 1))
+            err = "BVH2: primitive " + std::to_string(i) + " referenced " + std::to_string(seen[i]) + " times";
+    if (err.empty() && max_depth > s->bvh.depth2) err = "BVH2 deeper than its recorded depth";
+    // wide tree
+    std::fill(seen.begin(), seen.end(), 0);
+    int max_stack = 0;
+    std::function<B(int, int)> walk4 = [&](int ref, int pushes) -> B {
+        B u = empty();
+        if (!err.empty()) return u;
+        if (ref < 0) {
+            leaf(ref, u);
+            return u;
+        }
+        if (ref >= (int)n4.size()) {
+            err = "wide child index out of range";
+            return u;
+        }
+        const Node4Q& q = n4[ref];
+        uint32_t ex, ql[3], qh[3];
+        int refs[4], nc;
+        std::memcpy(&ex, &q.a.w, 4);
+        std::memcpy(&ql[0], &q.b.x, 4);
+        std::memcpy(&qh[0], &q.b.y, 4);
+        std::memcpy(&ql[1], &q.b.z, 4);
+        std::memcpy(&qh[1], &q.b.w, 4);
+        std::memcpy(&ql[2], &q.c.x, 4);
+        std::memcpy(&qh[2], &q.c.y, 4);
+        std::memcpy(&refs[0], &q.c.z, 4);
+        std::memcpy(&refs[1], &q.c.w, 4);
+        std::memcpy(&refs[2], &q.d.x, 4);
+        std::memcpy(&refs[3], &q.d.y, 4);
+        std::memcpy(&nc, &q.d.z, 4);
+        if (nc < 1 || nc > 4) {
+            err = "wide node with a bad child count";
+            return u;
+        }
+        max_stack = std::max(max_stack, pushes + nc - 1);
+        const double org[3] = {q.a.x, q.a.y, q.a.z};
+        for (int k = 0; k < nc; k++) {
+            const B sub = walk4(refs[k], pushes + nc - 1);
+            B box;
+            for (int a = 0; a < 3; a++) {
+                const double sc = std::ldexp(1.0, (int)((ex >> (8 * a)) & 255u) - 128);
+                box.lo[a] = org[a] + ((ql[a] >> (8 * k)) & 255u) * sc;
+                box.hi[a] = org[a] + ((qh[a] >> (8 * k)) & 255u) * sc;
+            }
+            if (err.empty() && !contains(box, sub)) err = "wide child box misses a primitive below it";
+            grow(u, sub);
+        }
+        return u;
+    };
+    if (err.empty() && nb > 0) walk4(s->bvh.root4, 0);
+    for (int i = 0; i < n && err.empty(); i++)
+        if (seen[i] != (H[i].kind == RT_PRIM_PLANE ? 0 : 1))
+            err = "wide tree: primitive " + std::to_string(i) + " referenced " + std::to_string(seen[i]) + " times";
+    if (err.empty() && max_stack > s->bvh.stack4) err = "wide tree needs more stack than recorded";
+    if (!err.empty()) {
+        set_error("rt_scene_check_bvh: " + err);
+        return RT_ERR_STATE;
+    }
+    return RT_OK;
+}
+
 int rt_abi_version(void) { return RTCORE_ABI_VERSION; }
 
 int rt_device_count(void)
@@ -718,11 +1018,19 @@ int rt_scene_create(const rt_scene_params* params, const rt_prim* prims, int32_t
     HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&s->ev0));
     HIP_TRY(hipEventCreate(&s->ev1));
+    using clk = std::chrono::steady_clock;
+    auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
+    const auto t0 = clk::now();
     s->host = prepare_prims(prims, n_prims);
-    s->sah = build_sah_bvh(s->host, n_prims > 256 ? 4 : 2);
-    s->bvh4 = build_bvh4(s->sah);
-    int rc = upload_scene(s.get());
+    const auto t1 = clk::now();
+    int rc = build_bvhs(s.get());
     if (rc != RT_OK) return rc;
+    const auto t2 = clk::now();
+    rc = upload_scene(s.get());
+    if (rc != RT_OK) return rc;
+    s->ms_prepare = ms(t1 - t0);
+    s->ms_bvh = ms(t2 - t1);
+    s->ms_upload = ms(clk::now() - t2);
     rc = resolve_traversal(s.get());
     if (rc != RT_OK) return rc;
     HIP_TRY(s->rays.reserve(1));
@@ -764,8 +1072,9 @@ int rt_scene_get_info(const rt_scene* s, rt_scene_info* info)
     info->n_prims = (int32_t)s->host.size();
     info->ref_bvh_nodes = (int32_t)s->ref.nodes.size();
     info->ref_bvh_depth = s->ref.depth;
-    info->sah_bvh_nodes = (int32_t)s->sah.nodes.size();
-    info->sah_bvh_depth = s->sah.depth;
+    info->sah_bvh_nodes = s->bvh.n_nodes2;
+    info->sah_bvh_depth = s->bvh.depth2;
+    info->bvh_builder = s->bvh.builder;
     info->traversal = s->resolved;
     info->device = s->device;
     info->device_bytes = s->device_bytes;

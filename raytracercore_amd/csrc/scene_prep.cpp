@@ -79,7 +79,7 @@ static double prim_extent(const HostPrim& p, Vec4d dir)
 std::vector<HostPrim> prepare_prims(const rt_prim* in, int n)
 {
     std::vector<HostPrim> out(n);
-    for (int i = 0; i < n; i++) {
+    parallel_for(n, [&](int i) {
         const rt_prim& a = in[i];
         HostPrim& p = out[i];
         p.kind = a.kind;
@@ -119,7 +119,7 @@ std::vector<HostPrim> prepare_prims(const rt_prim* in, int n)
         Vec4d lo = v4d(prim_extent(p, v4d(-1, 0, 0, 0)), prim_extent(p, v4d(0, -1, 0, 0)), prim_extent(p, v4d(0, 0, -1, 0)), 0);
         Vec4d hi = v4d(prim_extent(p, v4d(1, 0, 0, 0)), prim_extent(p, v4d(0, 1, 0, 0)), prim_extent(p, v4d(0, 0, 1, 0)), 0);
         p.box = box_make(sub(p.center_pt, lo), add(p.center_pt, hi));
-    }
+    });
     return out;
 }
 

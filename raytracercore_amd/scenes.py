@@ -1,4 +1,4 @@
-"""Procedural scenes of the measurement configs.
+"""Procedural scenes of the measurement configs and of the BVH tests.
 
 C4 ("M1M"): the bounce.txt Cornell room, light box and cameras, with the corner cut-out, cube,
 lens and spheres replaced by a displaced height field of 1001 x 501 vertices = 1,000,000
@@ -64,3 +64,22 @@ def mesh_scene_text(nx: int = 1001, ny: int = 501, seed: int = 42, bounce_text: 
 
         bounce_text = open(scene_path("bounce.txt")).read()
     return _room_header(bounce_text) + heightfield_text(nx, ny, seed)
+
+
+def soup_scene_text(n: int, seed: int) -> str:
+    """Random triangles and spheres (every fifth) over six orders of magnitude of size: a stress
+    case for BVH builders and the wide tree's 8-bit quantisation."""
+    rng = np.random.default_rng(seed)
+    lines = ["size 32 32", "camera 0 -50 0, 0 0 0, 0 0 1, 60"]
+    for i in range(n):
+        c = rng.uniform(-20, 20, 3)
+        s = 10.0 ** rng.uniform(-4, 1)
+        if i % 5 == 0:
+            lines.append(f"sphere {c[0]:.9g} {c[1]:.9g} {c[2]:.9g} {s:.9g}")
+        else:
+            for _ in range(3):
+                v = c + rng.normal(0, s, 3)
+                lines.append(f"vertex {v[0]:.9g} {v[1]:.9g} {v[2]:.9g}")
+            b = 3 * (i - i // 5 - 1)
+            lines.append(f"tri {b} {b + 1} {b + 2}")
+    return "\n".join(lines) + "\n"

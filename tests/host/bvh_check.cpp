@@ -7,7 +7,9 @@
 //     arithmetic) that contain every primitive box below that child;
 //   * never need more traversal-stack entries than the computed stack_need.
 // Prints "ok <n_prims> <bvh2 nodes> <wide nodes> <stack_need>" or the first failure.
+#include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -112,9 +114,18 @@ int main(int argc, char** argv)
         std::printf("parse error: %s\n", err.c_str());
         return 1;
     }
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     const std::vector<HostPrim> H = prepare_prims(ps.prims.data(), (int)ps.prims.size());
+    const auto t1 = clk::now();
     const SahBvh b2 = build_sah_bvh(H, H.size() > 256 ? 4 : 2);
+    const auto t2 = clk::now();
     const Bvh4 b4 = build_bvh4(b2);
+    const auto t3 = clk::now();
+    if (std::getenv("BVH_CHECK_TIME")) {
+        auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
+        std::fprintf(stderr, "prepare %.1f ms, sah %.1f ms, collapse %.1f ms\n", ms(t1 - t0), ms(t2 - t1), ms(t3 - t2));
+    }
     Ctx c;
     c.H = &H;
     c.b2 = &b2;

@@ -178,35 +178,17 @@ def bvh_check_bin():
     return os.path.join(ROOT, "raytracercore_amd", "csrc", "_obj", "bvh_check")
 
 
-def _soup(n, seed):
-    """Random triangles and spheres over six orders of magnitude of size (quantisation stress)."""
-    rng = np.random.default_rng(seed)
-    lines = ["size 32 32", "camera 0 -50 0, 0 0 0, 0 0 1, 60"]
-    for i in range(n):
-        c = rng.uniform(-20, 20, 3)
-        s = 10.0 ** rng.uniform(-4, 1)
-        if i % 5 == 0:
-            lines.append(f"sphere {c[0]:.9g} {c[1]:.9g} {c[2]:.9g} {s:.9g}")
-        else:
-            for k in range(3):
-                v = c + rng.normal(0, s, 3)
-                lines.append(f"vertex {v[0]:.9g} {v[1]:.9g} {v[2]:.9g}")
-            b = 3 * (i - i // 5 - 1)
-            lines.append(f"tri {b} {b + 1} {b + 2}")
-    return "\n".join(lines) + "\n"
-
-
 @pytest.mark.parametrize("name", ["bounce.txt", "die.txt", "SYNTH", "MESH200", "SOUP"])
 def test_wide_bvh_structure(rc, bvh_check_bin, tmp_path, name):
     """Host checks of the fast path's BVH: every primitive referenced once, every 4-wide node's
     8-bit dequantised child planes contain the primitives below them, stack bound honoured."""
     import subprocess
-    from raytracercore_amd.scenes import mesh_scene_text
+    from raytracercore_amd.scenes import mesh_scene_text, soup_scene_text
 
     if name == "MESH200":
         text = mesh_scene_text(nx=201, ny=101)
     elif name == "SOUP":
-        text = _soup(3000, 7)
+        text = soup_scene_text(3000, 7)
     else:
         text = _scene_text(rc, name)
     path = tmp_path / "scene.txt"
