@@ -32,9 +32,9 @@ enum : uint32_t {
 // other axes (in x, y, z order) and the one-sided culling rule folded into one factor:
 // a hit is kept iff cull * d[axis] <= 0 (0 = two-sided; Primitive.cs:56-61).
 struct alignas(16) RectRec {
+    float m1, m2;   // mid-points on the first and second remaining axes (one aligned SGPR pair:
+    float h1, h2;   // the in-plane test is one packed subtract), half-widths likewise
     float c;        // plane coordinate
-    float m1, h1;   // mid-point and half-width on the first remaining axis
-    float m2, h2;   // mid-point and half-width on the second remaining axis
     float cull;     // 0 two-sided, else +-1: sign(N[axis]), negated for Invert
     int32_t id;     // primitive ID
     int32_t sg;     // slot << 1 (the Best.sg of a hit)
