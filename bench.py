@@ -276,7 +276,8 @@ def main() -> int:
             "kernel_ms": round(avg_ms, 3),
             "roofline": roofline(args.config, fpr, bpr, my_rays_per_step, avg_ms),
             "path_stats": {"per_ray": {k: round(st[k], 3) for k in ("nodes", "tris", "sphs")},
-                           "lane_slots_per_ray": st["wave_iters_per_ray"]},
+                           "lane_slots_per_ray": st["wave_iters_per_ray"],
+                           "wave_cycles": st["cycles"]},
             "scene_build": {"builder": ["auto", "host", "gpu"][info.bvh_builder],
                             **{k: round(v, 2) for k, v in gpu.build_stats().items()}},
         }

@@ -139,7 +139,8 @@ __device__ __forceinline__ void hit_plane(const TestRec& R, int slot, V3 o, V3 d
 // Axis-aligned rectangle on plane `AXIS` (RectRec): the same hit as the Mirror parallelogram
 // test (u, v in [0, 1]^2) with the extents in world units.  id = 1 / d, oi = o / d.  The side
 // of the hit (Inside) is not tracked here: the shading step recomputes it from the normal.
-template <int AXIS>
+// SUB: oi holds o itself and t = (c - o) / d (one fewer live vector than the fma form)
+template <int AXIS, bool SUB = false>
 __device__ __forceinline__ void hit_rect(const RectRec& R, int sg, V3 o, V3 d, V3 id, V3 oi, int prev, Best& b)
 {
     const float ida = AXIS == 0 ? id.x : AXIS == 1 ? id.y : id.z;
@@ -147,7 +148,7 @@ __device__ __forceinline__ void hit_rect(const RectRec& R, int sg, V3 o, V3 d, V
     const float da = AXIS == 0 ? d.x : AXIS == 1 ? d.y : d.z;
     const float d1 = AXIS == 0 ? d.y : d.x, o1 = AXIS == 0 ? o.y : o.x;
     const float d2 = AXIS == 2 ? d.y : d.z, o2 = AXIS == 2 ? o.y : o.z;
-    const float t = fmaf(R.c, ida, -oia);
+    const float t = SUB ? (R.c - oia) * ida : fmaf(R.c, ida, -oia);
     // |p - mid| <= half on both in-plane axes (false for NaN)
     const bool in1 = fabsf(fmaf(t, d1, o1) - R.m1) <= R.h1;
     const bool in2 = fabsf(fmaf(t, d2, o2) - R.m2) <= R.h2;
@@ -158,28 +159,28 @@ __device__ __forceinline__ void hit_rect(const RectRec& R, int sg, V3 o, V3 d, V
     b.sg = ok ? sg : b.sg;
 }
 
-template <int AXIS>
+template <int AXIS, bool SUB = false>
 __device__ __forceinline__ void rect_group(const RectRec* __restrict__ r, int n, V3 o, V3 d, V3 id, V3 oi, int prev,
                                            Best& b)
 {
 #ifdef RT_EXP_RECT_UNROLL4
     for (; n >= 4; n -= 4, r += 4) {
         const RectRec r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
-        hit_rect<AXIS>(r0, r0.sg, o, d, id, oi, prev, b);
-        hit_rect<AXIS>(r1, r1.sg, o, d, id, oi, prev, b);
-        hit_rect<AXIS>(r2, r2.sg, o, d, id, oi, prev, b);
-        hit_rect<AXIS>(r3, r3.sg, o, d, id, oi, prev, b);
+        hit_rect<AXIS, SUB>(r0, r0.sg, o, d, id, oi, prev, b);
+        hit_rect<AXIS, SUB>(r1, r1.sg, o, d, id, oi, prev, b);
+        hit_rect<AXIS, SUB>(r2, r2.sg, o, d, id, oi, prev, b);
+        hit_rect<AXIS, SUB>(r3, r3.sg, o, d, id, oi, prev, b);
     }
 #endif
 #ifndef RT_EXP_RECT_NO_UNROLL
     for (; n >= 2; n -= 2, r += 2) {
         const RectRec r0 = r[0], r1 = r[1];
-        hit_rect<AXIS>(r0, r0.sg, o, d, id, oi, prev, b);
-        hit_rect<AXIS>(r1, r1.sg, o, d, id, oi, prev, b);
+        hit_rect<AXIS, SUB>(r0, r0.sg, o, d, id, oi, prev, b);
+        hit_rect<AXIS, SUB>(r1, r1.sg, o, d, id, oi, prev, b);
     }
-    if (n > 0) hit_rect<AXIS>(*r, r->sg, o, d, id, oi, prev, b);
+    if (n > 0) hit_rect<AXIS, SUB>(*r, r->sg, o, d, id, oi, prev, b);
 #else
-    for (; n > 0; n--, r++) hit_rect<AXIS>(*r, r->sg, o, d, id, oi, prev, b);
+    for (; n > 0; n--, r++) hit_rect<AXIS, SUB>(*r, r->sg, o, d, id, oi, prev, b);
 #endif
 }
 
@@ -210,19 +211,20 @@ __device__ __forceinline__ bool slab(float4 lo, float4 hi, V3 oi, V3 id, float t
 template <bool CULL, bool STATS>
 __device__ __forceinline__ void trace_brute(const PathScene& s, const GroupRec* __restrict__ groups,
                                             const TestRec* __restrict__ tests, const RectRec* __restrict__ rects,
-                                            const XformF* __restrict__ xf, V3 o, V3 d, int prev, Best& b,
-                                            unsigned& n_flat, unsigned& n_sph)
+                                            const FrameRec* __restrict__ frames, const XformF* __restrict__ xf, V3 o,
+                                            V3 d, int prev, Best& b, unsigned& n_flat, unsigned& n_sph)
 {
     const V3 id = v3(slab_rcp(d.x), slab_rcp(d.y), slab_rcp(d.z));
     const V3 oi = o * id;
-    for (int g = 0; g < s.n_groups; g++) {
+    const int n_groups = CULL ? s.n_groups : 1; // the flat order is one group (1/d and o/d die after its rects)
+    for (int g = 0; g < n_groups; g++) {
         const GroupRec G = groups[g];
         if (CULL) {
             float tn;
             if (!__any(slab(G.lo, G.hi, oi, id, b.t, tn))) continue;
         }
         if (STATS) { // primitive tests actually made (groups the wave skipped are not counted)
-            n_flat += G.n_rect[0] + G.n_rect[1] + G.n_rect[2] + (G.n_tri_sph & 0xFFFF);
+            n_flat += G.n_rect[0] + G.n_rect[1] + G.n_rect[2] + G.n_frame_rects + (G.n_tri_sph & 0xFFFF);
             n_sph += G.n_tri_sph >> 16;
         }
         const RectRec* r = rects + __float_as_int(G.lo.w);
@@ -231,6 +233,22 @@ __device__ __forceinline__ void trace_brute(const PathScene& s, const GroupRec* 
         rect_group<1>(r, G.n_rect[1], o, d, id, oi, prev, b);
         r += G.n_rect[1];
         rect_group<2>(r, G.n_rect[2], o, d, id, oi, prev, b);
+        // rectangles in a common affine frame: the ray mapped once, then the same rect tests (t is
+        // invariant under the map; a local d of 0 gives an infinite or NaN t, which never hits)
+#ifndef RT_EXP_NO_FRAMES
+        for (int f = G.frame_first; f < G.frame_first + G.n_frames; f++) {
+            const FrameRec F = frames[f];
+            const V3 lo = v3(dot4(F.r0, o), dot4(F.r1, o), dot4(F.r2, o));
+            const V3 ld = v3(dot3(F.r0, d), dot3(F.r1, d), dot3(F.r2, d));
+            const V3 lid = v3(rcp(ld.x), rcp(ld.y), rcp(ld.z));
+            const RectRec* fr = rects + F.rect_first;
+            rect_group<0, true>(fr, F.n_rect[0], lo, ld, lid, lo, prev, b);
+            fr += F.n_rect[0];
+            rect_group<1, true>(fr, F.n_rect[1], lo, ld, lid, lo, prev, b);
+            fr += F.n_rect[1];
+            rect_group<2, true>(fr, F.n_rect[2], lo, ld, lid, lo, prev, b);
+        }
+#endif
         int i = __float_as_int(G.hi.w);
         int end = i + (G.n_tri_sph & 0xFFFF);
         if (i < end) {
@@ -497,7 +515,7 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
     V3 pos = madd(S.d, b.t, S.o);
     const bool sph = kind == RT_PRIM_SPHERE;
     const uint32_t axis = (fl & F_AXIS_MASK) >> F_AXIS_SHIFT; // axis-aligned rectangle: on its plane
-    if (axis) gin = dot(S.d, xyz(P.d)) > 0.0f;                 // Moller-Trumbore's inside = d . N > 0
+    if (axis | (fl & F_FRAME_RECT)) gin = dot(S.d, xyz(P.d)) > 0.0f; // Moller-Trumbore's inside = d . N > 0
     pos.x = axis == 1 ? P.a.x : pos.x;
     pos.y = axis == 2 ? P.a.y : pos.y;
     pos.z = axis == 3 ? P.a.z : pos.z;
@@ -763,8 +781,9 @@ __device__ __forceinline__ void flush_counts(const Lane& L, const Counters& cnt,
 // (the scene's records arrive through scalar loads) and shades it.
 template <bool CULL, bool LDS, bool STATS>
 __global__ void __launch_bounds__(256, RT_PATH_WAVES)
-    path_kernel(PathScene s, CameraF cam, PathParams p, const TestRec* __restrict__ tests,
-                const RectRec* __restrict__ rects, const PrimF* __restrict__ prims_g, const NodeF* __restrict__ nodes,
+    path_kernel(PathScene s, const CameraF* __restrict__ camp, PathParams p, const TestRec* __restrict__ tests,
+                const RectRec* __restrict__ rects, const FrameRec* __restrict__ frames,
+                const PrimF* __restrict__ prims_g, const NodeF* __restrict__ nodes,
                 const Node4Q* __restrict__ nodes4, const GroupRec* __restrict__ groups, const XformF* __restrict__ xf,
                 const MatF* __restrict__ mats_g, const float4* __restrict__ vnormals)
 {
@@ -784,14 +803,21 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
     while (true) {
         unsigned long long t0 = 0, t1 = 0, t2 = 0;
         if (STATS) t0 = __builtin_readcyclecounter();
-        refill(L, S, p, s, cam, lane, total);
+        {
+            // the camera is read per iteration through scalar loads from an opaque pointer: that
+            // keeps the compiler from holding ~28 camera words in SGPRs for the whole kernel
+            // (they spilled, with the kernel's other arguments, into VGPR lanes and scratch)
+            const CameraF* cp = camp;
+            asm volatile("" : "+s"(cp));
+            refill(L, S, p, s, *cp, lane, total);
+        }
         if (!__any(L.active)) break;
         if (STATS) t1 = __builtin_readcyclecounter();
 #ifdef RT_EXP_DUP_START // cost experiment: a second camera sample on a copy
         if (L.live) {
             Sample S2 = S;
             S2.rng.k0 ^= (unsigned)L.rays;
-            start_sample(cam, L.fx, L.fy, S2);
+            start_sample(*camp, L.fx, L.fy, S2);
             exp_sink += S2.o.x + S2.d.y;
         }
 #endif
@@ -801,12 +827,12 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
             {
                 Best b2{__builtin_huge_valf(), -1, 0.0f, 0.0f};
                 unsigned u0 = 0, u1 = 0;
-            trace_brute<CULL, false>(s, groups, tests, rects, xf, S.o + v3(exp_sink * 1e-30f, 0, 0), S.d, S.prev, b2,
-                                     u0, u1);
+            trace_brute<CULL, false>(s, groups, tests, rects, frames, xf, S.o + v3(exp_sink * 1e-30f, 0, 0), S.d,
+                                     S.prev, b2, u0, u1);
                 exp_sink += b2.t;
             }
 #endif
-            trace_brute<CULL, STATS>(s, groups, tests, rects, xf, S.o, S.d, S.prev, b, cnt.tris, cnt.sphs);
+            trace_brute<CULL, STATS>(s, groups, tests, rects, frames, xf, S.o, S.d, S.prev, b, cnt.tris, cnt.sphs);
             for (int i = pln0; i < pln0 + s.n_pln; i++) hit_plane(tests[i], i, S.o, S.d, S.prev, b);
             if (STATS) t2 = __builtin_readcyclecounter();
 #ifdef RT_EXP_DUP_SHADE // cost experiment: a second bounce on a copy
@@ -841,8 +867,9 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
 // divergent shading code is paid once per batch of finished queries.
 template <int WIDTH, int STACK, bool LDS, bool STATS>
 __global__ void __launch_bounds__(256, RT_BVH_WAVES)
-    path_kernel_bvh(PathScene s, CameraF cam, PathParams p, const TestRec* __restrict__ tests,
-                    const RectRec* __restrict__ rects, const PrimF* __restrict__ prims_g,
+    path_kernel_bvh(PathScene s, const CameraF* __restrict__ camp, PathParams p, const TestRec* __restrict__ tests,
+                    const RectRec* __restrict__ rects, const FrameRec* __restrict__ frames,
+                    const PrimF* __restrict__ prims_g,
                     const NodeF* __restrict__ nodes, const Node4Q* __restrict__ nodes4,
                     const GroupRec* __restrict__ groups, const XformF* __restrict__ xf,
                     const MatF* __restrict__ mats_g, const float4* __restrict__ vnormals)
@@ -850,6 +877,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
     __shared__ int stack_mem[STACK * 256];
     extern __shared__ float4 lds_scene[];
     const TravStack stk{stack_mem + threadIdx.x, p.stack_ovf + blockIdx.x * 256 + threadIdx.x, (int)gridDim.x * 256};
+    const CameraF cam = *camp;
     const ShadeRecs R = stage_scene<LDS>(s, prims_g, mats_g, xf, lds_scene);
     const int lane = threadIdx.x & 63;
     const unsigned total = (unsigned)p.n_chunks * (unsigned)p.n_pad;
@@ -1036,7 +1064,7 @@ __global__ void colors_1spp_kernel(PathParams p, double* out)
     out[o + 2] = miss ? -1.0 : (double)v.z;
 }
 
-using PathKernel = void (*)(PathScene, CameraF, PathParams, const TestRec*, const RectRec*, const PrimF*,
+using PathKernel = void (*)(PathScene, const CameraF*, PathParams, const TestRec*, const RectRec*, const FrameRec*, const PrimF*,
                             const NodeF*, const Node4Q*, const GroupRec*, const XformF*, const MatF*, const float4*);
 
 template <bool CULL, bool LDS>
@@ -1111,7 +1139,7 @@ int path_blocks_per_cu(int variant, size_t dyn_lds, bool stats)
     return n;
 }
 
-hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& p, int variant, int grid_blocks,
+hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams& p, int variant, int grid_blocks,
                        hipStream_t stream, bool stats)
 {
     PathScene ps = make_path_scene(s);
@@ -1119,10 +1147,11 @@ hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& 
     if (kernel == 3) ps.root = s.root4; // the wide kernel walks the collapsed tree
     const bool grouped = kernel == 1, bvh = kernel >= 2;
     ps.n_groups = grouped ? s.n_groups_gr : 1;
-    CameraF ca = cam;
+    const CameraF* ca = d_cam;
     PathParams pa = p;
     const TestRec* tests = bvh ? s.tests_bvh : grouped ? s.tests_gr : s.tests_bf;
     const RectRec* rects = grouped ? s.rects_gr : s.rects_bf;
+    const FrameRec* frames = grouped ? s.frames_gr : s.frames_bf;
     const PrimF* prims = bvh ? s.prims_bvh : grouped ? s.prims_gr : s.prims_bf;
     const NodeF* nodes = s.nodes;
     const Node4Q* nodes4 = s.nodes4;
@@ -1130,7 +1159,7 @@ hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& 
     const XformF* xf = s.xf;
     const MatF* mats = s.mats;
     const float4* vn = s.vnormals;
-    void* args[] = {&ps, &ca, &pa, &tests, &rects, &prims, &nodes, &nodes4, &groups, &xf, &mats, &vn};
+    void* args[] = {&ps, &ca, &pa, &tests, &rects, &frames, &prims, &nodes, &nodes4, &groups, &xf, &mats, &vn};
     const size_t dyn = (variant & 1) ? path_lds_bytes(s) : 0;
     return hipLaunchKernel(reinterpret_cast<const void*>(pick(variant, stats)), dim3(grid_blocks), dim3(256), args, dyn,
                            stream);

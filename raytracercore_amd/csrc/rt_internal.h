@@ -25,6 +25,7 @@ enum : uint32_t {
     F_TRANSFORMED = 1u << 6,
     F_AXIS_SHIFT = 7,   // axis-aligned rectangle: (axis + 1) in bits 7-8, 0 = general
     F_AXIS_MASK = 3u << 7,
+    F_FRAME_RECT = 1u << 9, // brute-force slot tested as a rectangle of a FrameRec (shading: Inside from N . d)
 };
 
 // Axis-aligned rectangle (a Mirror parallelogram whose edges follow two coordinate axes, e.g.
@@ -38,6 +39,18 @@ struct alignas(16) RectRec {
     float cull;     // 0 two-sided, else +-1: sign(N[axis]), negated for Invert
     int32_t id;     // primitive ID
     int32_t sg;     // slot << 1 (the Best.sg of a hit)
+};
+
+// Parallelograms whose edges follow the axes of one common affine frame (the six faces of a
+// transformed `cube`, Cube.cs:90-116, whose vertices the loader bakes into world space,
+// Triangle.cs:68-74) are tested as axis-aligned rectangles in that frame: the ray is mapped
+// once per frame (rows r0..r2: world -> local, t is unchanged by an affine map), then each face
+// is a RectRec in local coordinates.  The rects of frame f are rects[rect_first ..) in local
+// axis order x | y | z.
+struct alignas(16) FrameRec {
+    float4 r0, r1, r2;          // local = (r_k . p + r_k.w)
+    int32_t rect_first;
+    int32_t n_rect[3];
 };
 
 // ---- exact fp64 scene (primary-ID pass) -----------------------------------------------
@@ -92,15 +105,19 @@ struct alignas(16) MatF {       // per primitive ID, 80 B
     float inv_shininess;        // 1 / Shininess (RandomShine's exponent)
 };
 
-// A group of the brute-force slot order (48 B): its primitives' box (fp32, rounded outward) and
-// typed ranges -- rects (x | y | z) in RectRec order from rect_first, then triangles and spheres
-// in slot order from tri_slot.  The grouped kernel skips a group when no lane of the wave meets
-// its box; the flat order is one group whose box is never tested.
+// A group of the brute-force slot order (64 B): its primitives' box (fp32, rounded outward) and
+// typed ranges -- world rects (x | y | z) in RectRec order from rect_first, then n_frames
+// FrameRecs from frame_first (their rects follow the world rects), then triangles and spheres in
+// slot order from tri_slot.  The grouped kernel skips a group when no lane of the wave meets its
+// box; the flat order is one group whose box is never tested.
 struct alignas(16) GroupRec {
     float4 lo;     // xyz, w = bitcast rect_first
     float4 hi;     // xyz, w = bitcast tri_slot
     int32_t n_rect[3];
     int32_t n_tri_sph; // n_tri | n_sph << 16
+    int32_t frame_first, n_frames;
+    int32_t n_frame_rects; // rect tests of the group's frames (statistics)
+    int32_t pad;
 };
 
 // Intersection record of the fp32 kernel (64 B), one per primitive slot:
@@ -230,17 +247,19 @@ struct DevScene {
     // fast set; slot order is [triangles | spheres | planes] for brute force and
     // [BVH leaf order | planes] for the BVH, with matching TestRec / PrimF arrays
     const TestRec* tests_bf;
-    const RectRec* rects_bf;    // slots [0, n_rect[0] + n_rect[1] + n_rect[2])
+    const RectRec* rects_bf;    // world rects of the groups, then their frames' rects
+    const FrameRec* frames_bf;
     const PrimF* prims_bf;
     const GroupRec* groups_bf;  // one group: the whole flat order
     // the grouped brute-force order (same records, group-major slot order)
     const TestRec* tests_gr;
     const RectRec* rects_gr;
+    const FrameRec* frames_gr;
     const PrimF* prims_gr;
     const GroupRec* groups_gr;
     int32_t n_groups_gr;
     int32_t n_rect[3];
-    int32_t n_tri, n_sph, n_pln; // n_tri counts general triangles only
+    int32_t n_tri, n_sph, n_pln; // n_tri counts general triangles (frame rects included), not world rects
     const TestRec* tests_bvh;
     const PrimF* prims_bvh;
     const NodeF* nodes;

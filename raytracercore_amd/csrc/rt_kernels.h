@@ -41,7 +41,7 @@ constexpr int kStackOverflow = 40; // = RT_STACK_OVF (kernels_path.hip)
 int path_wide_stack();              // LDS entries of the wide BVH kernel's stack (RT_WIDE_STACK)
 size_t path_lds_bytes(const DevScene& s);   // dynamic LDS of the staged (lds) variants
 // Launch the persistent kernel; stats counts node visits / primitive tests (slower build).
-hipError_t launch_path(const DevScene& s, const CameraF& cam, const PathParams& p, int variant, int grid_blocks,
+hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams& p, int variant, int grid_blocks,
                        hipStream_t stream, bool stats);
 int path_blocks_per_cu(int variant, size_t dyn_lds, bool stats);
 

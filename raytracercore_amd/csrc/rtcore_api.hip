@@ -114,10 +114,12 @@ struct rt_scene {
     DevBuf<PrimF> prims_bf, prims_bvh;
     DevBuf<TestRec> tests_bf, tests_bvh;
     DevBuf<RectRec> rects_bf;
+    DevBuf<FrameRec> frames_bf;
     DevBuf<GroupRec> groups_bf;
     DevBuf<PrimF> prims_gr;
     DevBuf<TestRec> tests_gr;
     DevBuf<RectRec> rects_gr;
+    DevBuf<FrameRec> frames_gr;
     DevBuf<GroupRec> groups_gr;
     double grouped_measured = 0; // calibrated brute-force cost ratio flat / grouped (AUTO picks grouped above 1.25)
     DevBuf<NodeF> nodes;
@@ -141,6 +143,7 @@ struct rt_scene {
     DevBuf<unsigned long long> stats_buf;
     CameraD camd{};
     CameraF camf{};
+    DevBuf<CameraF> camf_d;     // the path kernels read the camera from device memory (not kernel arguments)
     bool has_camera = false;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -292,21 +295,123 @@ int upload_scene(rt_scene* s)
         r.sg = 0; // set once the slot is known
         return r;
     };
-    // Brute-force slot orders: groups of primitives, each [x-rects | y-rects | z-rects | triangles |
-    // spheres], then the planes.  The flat order is one group of everything; the grouped order
-    // cuts the SAH BVH into subtrees of at most kGroupMax primitives.
-    struct BruteOrder {
-        std::vector<PrimF> prims;
-        std::vector<TestRec> tests;
-        std::vector<RectRec> rects;
-        std::vector<GroupRec> groups;
-        int nr[3] = {0, 0, 0}, nt = 0, ns = 0;
-    };
     std::vector<int> kind_of(n);
     for (int i = 0; i < n; i++) {
         const int ax = rect_axis(i);
         kind_of[i] = ax >= 0 ? ax : (H[i].kind == RT_PRIM_TRIANGLE ? 3 : H[i].kind == RT_PRIM_SPHERE ? 4 : 5);
     }
+    // Frames: the general Mirror parallelograms of a group whose edges run along the three edge
+    // directions of one affine frame (a transformed cube's faces) become rectangles in that frame
+    // (FrameRec); a frame is used when it collects at least two faces.
+    struct FrameB {
+        Vec4d b[3];
+        bool b2_set = false; // b[2] came from an edge (else it is the first face's normal)
+        Vec4d org;
+        std::vector<int> face[3]; // faces on local plane k (edges along the other two axes)
+    };
+    auto parallel = [](const Vec4d& a, const Vec4d& b) {
+        const Vec4d c = cross_s(a, b);
+        const double aa = dot_s(a, a), bb = dot_s(b, b);
+        return aa > 0 && bb > 0 && dot_s(c, c) <= 1e-18 * aa * bb;
+    };
+    auto find_frames = [&](const std::vector<int>& ids) {
+        std::vector<FrameB> fr;
+        for (int i : ids) {
+            const HostPrim& p = H[i];
+            if (kind_of[i] != 3 || !(p.flags & F_MIRROR) || (p.flags & F_HASNORMALS)) continue;
+            bool placed = false;
+            for (auto& F : fr) {
+                int k1 = -1, k2 = -1;
+                for (int k = 0; k < 3; k++) {
+                    if (k1 < 0 && parallel(p.e01, F.b[k])) k1 = k;
+                    if (k2 < 0 && parallel(p.e02, F.b[k])) k2 = k;
+                }
+                if (!F.b2_set && F.face[0].empty() && F.face[1].empty()) { // third axis still open
+                    if (k1 >= 0 && k1 != 2 && k2 < 0) {
+                        F.b[2] = p.e02;
+                        k2 = 2;
+                    } else if (k2 >= 0 && k2 != 2 && k1 < 0) {
+                        F.b[2] = p.e01;
+                        k1 = 2;
+                    }
+                    if (k1 == 2 || k2 == 2) F.b2_set = true;
+                }
+                if (k1 >= 0 && k2 >= 0 && k1 != k2) {
+                    F.face[3 - k1 - k2].push_back(i);
+                    placed = true;
+                    break;
+                }
+            }
+            if (!placed) {
+                FrameB F;
+                F.b[0] = p.e01;
+                F.b[1] = p.e02;
+                F.b[2] = cross_s(p.e01, p.e02);
+                F.org = p.v[0];
+                F.face[2].push_back(i);
+                fr.push_back(F);
+            }
+        }
+        std::vector<FrameB> keep;
+        for (auto& F : fr)
+            if (F.face[0].size() + F.face[1].size() + F.face[2].size() >= 2) keep.push_back(F);
+        return keep;
+    };
+    // local rows (world -> frame) of F: the inverse of [b0 b1 b2] applied to p - org
+    auto frame_rows = [&](const FrameB& F, double M[3][4]) {
+        const Vec4d c0 = cross_s(F.b[1], F.b[2]), c1 = cross_s(F.b[2], F.b[0]), c2 = cross_s(F.b[0], F.b[1]);
+        const double det = dot_s(F.b[0], c0);
+        const Vec4d rows[3] = {c0, c1, c2};
+        for (int k = 0; k < 3; k++) {
+            M[k][0] = rows[k].x / det;
+            M[k][1] = rows[k].y / det;
+            M[k][2] = rows[k].z / det;
+            M[k][3] = -(M[k][0] * F.org.x + M[k][1] * F.org.y + M[k][2] * F.org.z);
+        }
+    };
+    auto frame_rect = [&](const FrameB& F, const double M[3][4], int i, int k) {
+        const HostPrim& p = H[i];
+        auto loc = [&](double x, double y, double z, int a) { return M[a][0] * x + M[a][1] * y + M[a][2] * z + M[a][3]; };
+        const Vec4d v0 = p.v[0], e1 = p.e01, e2 = p.e02;
+        const double cx[4] = {v0.x, v0.x + e1.x, v0.x + e2.x, v0.x + e1.x + e2.x};
+        const double cy[4] = {v0.y, v0.y + e1.y, v0.y + e2.y, v0.y + e1.y + e2.y};
+        const double cz[4] = {v0.z, v0.z + e1.z, v0.z + e2.z, v0.z + e1.z + e2.z};
+        const int a1 = k == 0 ? 1 : 0, a2 = k == 2 ? 1 : 2;
+        double c = 0, lo1 = 1e300, hi1 = -1e300, lo2 = 1e300, hi2 = -1e300;
+        for (int j = 0; j < 4; j++) {
+            c += 0.25 * loc(cx[j], cy[j], cz[j], k);
+            const double q1 = loc(cx[j], cy[j], cz[j], a1), q2 = loc(cx[j], cy[j], cz[j], a2);
+            lo1 = std::min(lo1, q1);
+            hi1 = std::max(hi1, q1);
+            lo2 = std::min(lo2, q2);
+            hi2 = std::max(hi2, q2);
+        }
+        RectRec r;
+        r.c = (float)c;
+        r.m1 = (float)(0.5 * (lo1 + hi1));
+        r.m2 = (float)(0.5 * (lo2 + hi2));
+        // half-widths padded by 2^-21 relative: the fp32 frame rows move the shared edges of
+        // neighbouring faces by about an ulp, and a padded edge is met by both faces (closest wins)
+        r.h1 = (float)(0.5 * (hi1 - lo1) + (std::fabs(0.5 * (lo1 + hi1)) + 0.5 * (hi1 - lo1)) * 4.76837158203125e-07);
+        r.h2 = (float)(0.5 * (hi2 - lo2) + (std::fabs(0.5 * (lo2 + hi2)) + 0.5 * (hi2 - lo2)) * 4.76837158203125e-07);
+        // gin = N . d > 0 = sign(N . b_k) * d_local[k] > 0; the culling factor as for world rects
+        const float ns = dot_s(p.n, F.b[k]) > 0 ? 1.0f : -1.0f;
+        r.cull = (p.flags & F_TWOSIDED) ? 0.0f : ((p.flags & F_INVERT) ? -ns : ns);
+        r.id = i;
+        r.sg = 0;
+        return r;
+    };
+    // Brute-force slot orders: groups of primitives, each [x-rects | y-rects | z-rects | frame
+    // rects | triangles | spheres], then the planes.  The flat order is one group of everything;
+    // the grouped order cuts the SAH BVH into subtrees of at most kGroupMax primitives.
+    struct BruteOrder {
+        std::vector<PrimF> prims;
+        std::vector<TestRec> tests;
+        std::vector<RectRec> rects;
+        std::vector<FrameRec> frames;
+        std::vector<GroupRec> groups;
+        int nr[3] = {0, 0, 0}, nt = 0, ns = 0;
+    };
     auto fbox = [&](const std::vector<int>& ids, float lo[3], float hi[3]) {
         for (int k = 0; k < 3; k++) {
             lo[k] = __builtin_huge_valf();
@@ -332,10 +437,47 @@ int upload_scene(rt_scene* s)
             const int rect_first = (int)o.rects.size();
             int cnt[5] = {0, 0, 0, 0, 0};
             int tri_slot = 0;
+            const std::vector<FrameB> frames = find_frames(g);
+            std::vector<char> in_frame(n, 0);
+            for (const auto& F : frames)
+                for (int k = 0; k < 3; k++)
+                    for (int i : F.face[k]) in_frame[i] = 1;
+            auto push_slot = [&](int i, PrimF f) {
+                o.prims.push_back(f);
+                o.tests.push_back(testrec(i));
+            };
             for (int kind = 0; kind < 5; kind++) {
-                if (kind == 3) tri_slot = (int)o.prims.size();
+                if (kind == 3) { // the frames' rects, then the remaining triangles
+                    G.frame_first = (int)o.frames.size();
+                    G.n_frames = (int)frames.size();
+                    for (const auto& F : frames) {
+                        double M[3][4];
+                        frame_rows(F, M);
+                        FrameRec R;
+                        std::memset(&R, 0, sizeof R);
+                        float4* rows[3] = {&R.r0, &R.r1, &R.r2};
+                        for (int k = 0; k < 3; k++)
+                            *rows[k] = make_float4((float)M[k][0], (float)M[k][1], (float)M[k][2], (float)M[k][3]);
+                        R.rect_first = (int)o.rects.size();
+                        for (int k = 0; k < 3; k++) {
+                            R.n_rect[k] = (int)F.face[k].size();
+                            for (int i : F.face[k]) {
+                                o.rects.push_back(frame_rect(F, M, i, k));
+                                o.rects.back().sg = (int)o.prims.size() << 1;
+                                PrimF f = primf(i);
+                                const uint32_t fl = H[i].flags | F_FRAME_RECT;
+                                std::memcpy(&f.b.w, &fl, 4);
+                                push_slot(i, f);
+                                G.n_frame_rects++;
+                                o.nt++;
+                            }
+                        }
+                        o.frames.push_back(R);
+                    }
+                    tri_slot = (int)o.prims.size();
+                }
                 for (int i : g) {
-                    if (kind_of[i] != kind) continue;
+                    if (kind_of[i] != kind || (kind == 3 && in_frame[i])) continue;
                     PrimF f = primf(i);
                     if (kind < 3) {
                         const uint32_t fl = p_flags_with_axis(H[i].flags, kind);
@@ -347,8 +489,7 @@ int upload_scene(rt_scene* s)
                         (kind == 3 ? o.nt : o.ns)++;
                     }
                     cnt[kind]++;
-                    o.prims.push_back(f);
-                    o.tests.push_back(testrec(i));
+                    push_slot(i, f);
                 }
             }
             G.lo = make_float4(lo[0], lo[1], lo[2], as_f(rect_first));
@@ -364,6 +505,7 @@ int upload_scene(rt_scene* s)
             }
         o.tests.push_back(TestRec{}); // spare records: loops may load one past a range
         o.rects.push_back(RectRec{});
+        o.frames.push_back(FrameRec{});
         return o;
     };
     std::vector<int> all;
@@ -467,10 +609,12 @@ int upload_scene(rt_scene* s)
     HIP_TRY(s->prims_bf.upload(flat.prims));
     HIP_TRY(s->tests_bf.upload(flat.tests));
     HIP_TRY(s->rects_bf.upload(flat.rects));
+    HIP_TRY(s->frames_bf.upload(flat.frames));
     HIP_TRY(s->groups_bf.upload(flat.groups));
     HIP_TRY(s->prims_gr.upload(grouped.prims));
     HIP_TRY(s->tests_gr.upload(grouped.tests));
     HIP_TRY(s->rects_gr.upload(grouped.rects));
+    HIP_TRY(s->frames_gr.upload(grouped.frames));
     HIP_TRY(s->groups_gr.upload(grouped.groups));
     if (s->bvh.builder != RT_BVH_BUILDER_GPU) {
         HIP_TRY(s->prims_bvh.upload(bv));
@@ -492,10 +636,12 @@ int upload_scene(rt_scene* s)
     d.tests_bf = s->tests_bf.p;
     d.tests_bvh = s->tests_bvh.p;
     d.rects_bf = s->rects_bf.p;
+    d.frames_bf = s->frames_bf.p;
     d.prims_bf = s->prims_bf.p;
     d.groups_bf = s->groups_bf.p;
     d.tests_gr = s->tests_gr.p;
     d.rects_gr = s->rects_gr.p;
+    d.frames_gr = s->frames_gr.p;
     d.prims_gr = s->prims_gr.p;
     d.groups_gr = s->groups_gr.p;
     d.n_groups_gr = (int)grouped.groups.size();
@@ -704,7 +850,7 @@ int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t
         p.stack_ovf = s->stack_ovf.p;
     }
     HIP_TRY(hipEventRecord(s->ev0, stream));
-    HIP_TRY(launch_path(s->dev, s->camf, p, s->variant, grid, stream, s->stats_on));
+    HIP_TRY(launch_path(s->dev, s->camf_d.p, p, s->variant, grid, stream, s->stats_on));
     HIP_TRY(hipEventRecord(s->ev1, stream));
     return RT_OK;
 }
@@ -1044,9 +1190,13 @@ int rt_scene_set_camera(rt_scene* s, const rt_camera* cam)
         set_error("rt_scene_set_camera: bad argument");
         return RT_ERR_ARG;
     }
-    camera_init(*cam, s->params.width, s->params.height, s->camd, s->camf);
-    s->has_camera = true;
     HIP_TRY(hipSetDevice(s->device));
+    camera_init(*cam, s->params.width, s->params.height, s->camd, s->camf);
+    // launches of the previous camera may still be in flight on any stream
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(s->camf_d.reserve(1));
+    HIP_TRY(hipMemcpy(s->camf_d.p, &s->camf, sizeof(CameraF), hipMemcpyHostToDevice));
+    s->has_camera = true;
     return calibrate_grouping(s);
 }
 

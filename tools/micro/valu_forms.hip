@@ -1,0 +1,92 @@
+// Microbenchmark: issue cost (cycles per wave64 instruction per SIMD, many waves resident) of
+// VALU encodings on gfx950, isolating SGPR operands, VOP2 accumulate forms and compares.
+// Vector instructions only.  usage: valu_forms
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#define N 16
+#define ITERS 1024
+
+#define KASM(NAME, INSTR, ...)                                                             \
+    __global__ void __launch_bounds__(256) NAME(float* out, float a, float b)              \
+    {                                                                                      \
+        float x[N];                                                                        \
+        for (int i = 0; i < N; i++) x[i] = threadIdx.x * 1e-3f + i;                        \
+        float bv = b + threadIdx.x * 1e-9f, cv = a + threadIdx.x * 1e-9f;                  \
+        for (int it = 0; it < ITERS; it++)                                                 \
+            _Pragma("unroll") for (int i = 0; i < N; i++) asm volatile(INSTR : __VA_ARGS__);\
+        float s = 0;                                                                       \
+        for (int i = 0; i < N; i++) s += x[i];                                             \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = s + bv + cv;                          \
+    }
+
+KASM(k_fma_vvv, "v_fma_f32 %0, %1, %2, %0", "+v"(x[i]) : "v"(cv), "v"(bv))
+KASM(k_fma_svv, "v_fma_f32 %0, %1, %2, %0", "+v"(x[i]) : "s"(a), "v"(bv))
+KASM(k_fmac_vv, "v_fmac_f32_e32 %0, %1, %2", "+v"(x[i]) : "v"(cv), "v"(bv))
+KASM(k_fmac_sv, "v_fmac_f32_e32 %0, %1, %2", "+v"(x[i]) : "s"(a), "v"(bv))
+KASM(k_add_vv, "v_add_f32_e32 %0, %1, %0", "+v"(x[i]) : "v"(bv))
+KASM(k_add_sv, "v_add_f32_e32 %0, %1, %0", "+v"(x[i]) : "s"(a))
+KASM(k_add_e64_sv, "v_add_f32_e64 %0, %1, %0", "+v"(x[i]) : "s"(a))
+KASM(k_mul_sv, "v_mul_f32_e32 %0, %1, %0", "+v"(x[i]) : "s"(a))
+KASM(k_sub_abs_v, "v_sub_f32_e64 %0, |%0|, %1", "+v"(x[i]) : "v"(bv))
+KASM(k_cmp_vcc, "v_cmp_lt_f32_e32 vcc, %0, %1", "+v"(x[i]) : "v"(bv) : "vcc")
+KASM(k_cmp_e64, "v_cmp_lt_f32_e64 s[40:41], %0, %1", "+v"(x[i]) : "v"(bv) : "s40", "s41")
+KASM(k_cmp_e64_s, "v_cmp_lt_f32_e64 s[40:41], %0, %1", "+v"(x[i]) : "s"(a) : "s40", "s41")
+KASM(k_cnd_e64, "v_cndmask_b32_e64 %0, %0, %1, s[40:41]", "+v"(x[i]) : "v"(bv) : "s40", "s41")
+KASM(k_cnd_vcc, "v_cndmask_b32_e32 %0, %0, %1, vcc", "+v"(x[i]) : "v"(bv) : "vcc")
+KASM(k_xor_vv, "v_xor_b32_e32 %0, %1, %0", "+v"(x[i]) : "v"(bv))
+KASM(k_xor_sv, "v_xor_b32_e32 %0, %1, %0", "+v"(x[i]) : "s"(a))
+KASM(k_max_vv, "v_max_f32_e32 %0, %1, %0", "+v"(x[i]) : "v"(bv))
+KASM(k_max3_vvv, "v_max3_f32 %0, %1, %2, %0", "+v"(x[i]) : "v"(bv), "v"(cv))
+KASM(k_med3_vvv, "v_med3_f32 %0, %1, %2, %0", "+v"(x[i]) : "v"(bv), "v"(cv))
+KASM(k_pkfma_vvv, "v_pk_fma_f32 %0, %1, %2, %0", "+v"(*(double*)&x[i & ~1]) : "v"(*(double*)&x[(i + 2) & 15]), "v"(*(double*)&x[(i + 4) & 15]))
+KASM(k_pkadd_vv, "v_pk_add_f32 %0, %1, %0", "+v"(*(double*)&x[i & ~1]) : "v"(*(double*)&x[(i + 2) & 15]))
+KASM(k_mov_sv, "v_mov_b32_e32 %0, %1", "=v"(x[i]) : "s"(a))
+
+typedef void (*kfn)(float*, float, float);
+static void run(const char* name, kfn k, float* out)
+{
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    const int blocks = 8192;
+    float ms = 0;
+    for (int rep = 0; rep < 2; rep++) {
+        hipEventRecord(e0);
+        k<<<blocks, 256>>>(out, 0.999f, 0.001f);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        hipEventElapsedTime(&ms, e0, e1);
+    }
+    const double winstr = blocks * 4.0 * ITERS * N;
+    printf("%-14s %.3f ms  %.2f cycles per wave-instruction per SIMD (at 2.4 GHz)\n", name, ms,
+           ms * 1e-3 * 2.4e9 / (winstr / 1024.0));
+}
+#define RUN(k) run(#k, k, out)
+int main()
+{
+    float* out;
+    hipMalloc(&out, 256 * 8192 * 4);
+    RUN(k_fma_vvv);
+    RUN(k_fma_svv);
+    RUN(k_fmac_vv);
+    RUN(k_fmac_sv);
+    RUN(k_add_vv);
+    RUN(k_add_sv);
+    RUN(k_add_e64_sv);
+    RUN(k_mul_sv);
+    RUN(k_sub_abs_v);
+    RUN(k_cmp_vcc);
+    RUN(k_cmp_e64);
+    RUN(k_cmp_e64_s);
+    RUN(k_cnd_e64);
+    RUN(k_cnd_vcc);
+    RUN(k_xor_vv);
+    RUN(k_xor_sv);
+    RUN(k_max_vv);
+    RUN(k_max3_vvv);
+    RUN(k_med3_vvv);
+    RUN(k_pkfma_vvv);
+    RUN(k_pkadd_vv);
+    RUN(k_mov_sv);
+    return 0;
+}
