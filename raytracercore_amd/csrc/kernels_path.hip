@@ -459,7 +459,11 @@ __device__ __forceinline__ void start_sample(const CameraF& cam, int x, int y, S
     const Ray3 r = camera_ray(cam, sx, sy);
     S.o = r.o;
     S.d = r.d;
+#ifdef RT_EXP_NO_DOF
+    if (false) {
+#else
     if (cam.dof != 0.0f) {
+#endif
         const V3 focus = madd(r.d, cam.focal_length - cam.image_plane, r.o);
         const float dist = fsqrt(next_u(S.rng)) * cam.dof;
         const float turn = next_u(S.rng);
@@ -672,7 +676,8 @@ __device__ __forceinline__ void lane_init(Lane& L)
 }
 
 // Lanes without a sample in flight close finished items and take new ones from the wave's
-// pool (one atomic per 64 items), then start the next camera sample of their item.
+// pool (one atomic per p.pool items: chunks of one 8x8 block), then start the next camera sample
+// of their item.
 __device__ __forceinline__ void refill(Lane& L, Sample& S, const PathParams& p, const PathScene& s, const CameraF& cam, int lane,
                                       unsigned total)
 {
@@ -686,7 +691,7 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const PathParams& p, 
         const unsigned k = (unsigned)__popcll(m), avail = L.pool_end - L.pool_next;
         unsigned fresh = 0;
         if (k > avail) { // wave-uniform: one atomic refills the pool
-            if (lane == 0) fresh = atomicAdd(p.counter, 64u);
+            if (lane == 0) fresh = atomicAdd(p.counter, (unsigned)p.pool);
             fresh = __builtin_amdgcn_readfirstlane(fresh);
         }
         if (need) {
@@ -717,7 +722,7 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const PathParams& p, 
         }
         if (k > avail) {
             L.pool_next = fresh + (k - avail);
-            L.pool_end = fresh + 64u;
+            L.pool_end = fresh + (unsigned)p.pool;
         } else {
             L.pool_next += k;
         }
@@ -832,7 +837,9 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
                 exp_sink += b2.t;
             }
 #endif
+#ifndef RT_EXP_NO_TRACE // cost experiment: every camera ray misses (per-sample overhead alone)
             trace_brute<CULL, STATS>(s, groups, tests, rects, frames, xf, S.o, S.d, S.prev, b, cnt.tris, cnt.sphs);
+#endif
             for (int i = pln0; i < pln0 + s.n_pln; i++) hit_plane(tests[i], i, S.o, S.d, S.prev, b);
             if (STATS) t2 = __builtin_readcyclecounter();
 #ifdef RT_EXP_DUP_SHADE // cost experiment: a second bounce on a copy

@@ -17,6 +17,8 @@ struct PathParams {
     int blocks_x;               // 8x8 pixel blocks per tile row
     int n_pad;                  // padded pixels per chunk (blocks * 64)
     int refill;                 // BVH kernel: waiting lanes (of 64) that trigger the shading phase
+    int pool;                   // work items a wave takes per atomic: 64 x a power of two <= n_chunks
+                                // (all from one 8x8 block, so a wave's lanes stay on neighbouring pixels)
     float inv_blocks_x;         // fp32 reciprocal for the item decode
     unsigned long long seed;
     rt_key2 seed_key;           // rt_rng_seed_key(seed) (rtcore_rng.h)

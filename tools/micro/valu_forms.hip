@@ -42,6 +42,32 @@ KASM(k_pkfma_vvv, "v_pk_fma_f32 %0, %1, %2, %0", "+v"(*(double*)&x[i & ~1]) : "v
 KASM(k_pkadd_vv, "v_pk_add_f32 %0, %1, %0", "+v"(*(double*)&x[i & ~1]) : "v"(*(double*)&x[(i + 2) & 15]))
 KASM(k_mov_sv, "v_mov_b32_e32 %0, %1", "=v"(x[i]) : "s"(a))
 
+KASM(k_mullo_u32, "v_mul_lo_u32 %0, %0, %1", "+v"(x[i]) : "v"(bv))
+KASM(k_mulhi_u32, "v_mul_hi_u32 %0, %0, %1", "+v"(x[i]) : "v"(bv))
+KASM(k_mul_u24, "v_mul_u32_u24_e32 %0, %0, %1", "+v"(x[i]) : "v"(bv))
+KASM(k_mad_u24, "v_mad_u32_u24 %0, %0, %1, %2", "+v"(x[i]) : "v"(bv), "v"(cv))
+KASM(k_xad_u32, "v_xad_u32 %0, %0, %1, %2", "+v"(x[i]) : "v"(bv), "v"(cv))
+KASM(k_lshl_add, "v_lshl_add_u32 %0, %0, 3, %1", "+v"(x[i]) : "v"(bv))
+KASM(k_lshr_b32, "v_lshrrev_b32_e32 %0, 16, %0", "+v"(x[i]))
+KASM(k_alignbit, "v_alignbit_b32 %0, %0, %1, 13", "+v"(x[i]) : "v"(bv))
+KASM(k_bfe_u32, "v_bfe_u32 %0, %0, 8, 8", "+v"(x[i]))
+KASM(k_cvt_f32_u32, "v_cvt_f32_u32_e32 %0, %0", "+v"(x[i]))
+KASM(k_sin, "v_sin_f32_e32 %0, %0", "+v"(x[i]))
+KASM(k_exp, "v_exp_f32_e32 %0, %0", "+v"(x[i]))
+KASM(k_sqrt, "v_sqrt_f32_e32 %0, %0", "+v"(x[i]))
+KASM(k_fma_lit, "v_fmaak_f32 %0, %0, %1, 0x3f000000", "+v"(x[i]) : "v"(bv))
+KASM(k_add_inl, "v_add_f32_e32 %0, 0.5, %0", "+v"(x[i]))
+KASM(k_cnd_sgpr_pair, "v_cndmask_b32_e64 %0, %0, %1, s[40:41]", "+v"(x[i]) : "v"(bv) : "s40", "s41")
+KASM(k_readlane, "v_readlane_b32 s40, %0, 3", "+v"(x[i]) :: "s40")
+KASM(k_and_or, "v_and_or_b32 %0, %0, %1, %2", "+v"(x[i]) : "v"(bv), "v"(cv))
+KASM(k_min_f32, "v_min_f32_e32 %0, %0, %1", "+v"(x[i]) : "v"(bv))
+KASM(k_med3_i32, "v_med3_i32 %0, %0, %1, %2", "+v"(x[i]) : "v"(bv), "v"(cv))
+KASM(k_min_u32, "v_min_u32_e32 %0, %0, %1", "+v"(x[i]) : "v"(bv))
+KASM(k_sub_u32, "v_sub_u32_e32 %0, %0, %1", "+v"(x[i]) : "v"(bv))
+KASM(k_ldexp, "v_ldexp_f32 %0, %0, %1", "+v"(x[i]) : "v"(bv))
+KASM(k_dot2, "v_dot2_f32_f16 %0, %0, %1, %2", "+v"(x[i]) : "v"(bv), "v"(cv))
+KASM(k_cmpx, "v_cmp_class_f32_e64 s[40:41], %0, %1", "+v"(x[i]) : "v"(bv) : "s40", "s41")
+
 typedef void (*kfn)(float*, float, float);
 static void run(const char* name, kfn k, float* out)
 {
@@ -85,8 +111,31 @@ int main()
     RUN(k_max_vv);
     RUN(k_max3_vvv);
     RUN(k_med3_vvv);
-    RUN(k_pkfma_vvv);
-    RUN(k_pkadd_vv);
+    RUN(k_mullo_u32);
+    RUN(k_mulhi_u32);
+    RUN(k_mul_u24);
+    RUN(k_mad_u24);
+    RUN(k_xad_u32);
+    RUN(k_lshl_add);
+    RUN(k_lshr_b32);
+    RUN(k_alignbit);
+    RUN(k_bfe_u32);
+    RUN(k_cvt_f32_u32);
+    RUN(k_sin);
+    RUN(k_exp);
+    RUN(k_sqrt);
+    RUN(k_fma_lit);
+    RUN(k_add_inl);
+    RUN(k_cnd_sgpr_pair);
+    RUN(k_readlane);
+    RUN(k_and_or);
+    RUN(k_min_f32);
+    RUN(k_med3_i32);
+    RUN(k_min_u32);
+    RUN(k_sub_u32);
+    RUN(k_ldexp);
+    RUN(k_dot2);
+    RUN(k_cmpx);
     RUN(k_mov_sv);
     return 0;
 }
