@@ -525,13 +525,8 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
     pos.z = axis == 3 ? P.a.z : pos.z;
     V3 n = sph ? (pos - xyz(P.a)) * P.b.y : xyz(P.d);
     if (fl & (F_TRANSFORMED | F_HASNORMALS)) {
-        if (sph) { // ellipsoid: the hit in object space (b.u is the object-space distance)
-            const XformF& X = xfs[__float_as_int(P.b.z)];
-            const V3 oo = xf_point(X.to_world, S.o);
-            const V3 dd = normalize(xf_dir(X.to_world, S.d));
-            const V3 op = madd(dd, b.u, oo);
-            pos = xf_point(X.to_obj, op);
-            n = normalize(xf_dir(X.to_normal, (op - xyz(P.a)) * P.b.y));
+        if (sph) { // ellipsoid: the world normal is an affine map of the world hit point
+            n = normalize(xf_point(xfs[__float_as_int(P.b.z)].normal, pos));
         } else { // Triangle.GetNormal quirk: Normal is never set -> NaN when inside
             const float4* vn = vnormals + 3 * id;
             n = normalize(madd(xyz(vn[2]), b.u + b.v, madd(xyz(vn[1]), b.v, xyz(vn[0]) * b.u)));
@@ -639,7 +634,8 @@ __device__ __forceinline__ ShadeRecs stage_scene(const PathScene& s, const PrimF
                                                  const XformF* xf, float4* lds_scene)
 {
     if (!LDS) return ShadeRecs{prims_g, mats_g, xf};
-    const int n_p = s.n_slots * 4, n_m = s.n_ids * 5, n_x = s.n_xf * 9;
+    const int n_p = s.n_slots * (int)(sizeof(PrimF) / 16), n_m = s.n_ids * (int)(sizeof(MatF) / 16),
+              n_x = s.n_xf * (int)(sizeof(XformF) / 16);
     const float4* gp = reinterpret_cast<const float4*>(prims_g);
     const float4* gm = reinterpret_cast<const float4*>(mats_g);
     const float4* gx = reinterpret_cast<const float4*>(xf);

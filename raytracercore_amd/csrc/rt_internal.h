@@ -88,10 +88,10 @@ struct alignas(16) PrimF {      // 64 B
     float4 d; // tri and plane: N.xyz, 0
 };
 
-struct alignas(16) XformF {     // rows 0-2 of each 4x4 (last row is 0 0 0 1)
-    float4 to_world[3];
-    float4 to_obj[3];
-    float4 to_normal[3];
+struct alignas(16) XformF {     // rows 0-2 (last row is 0 0 0 1)
+    float4 to_world[3];         // Sphere.MatrixToWorld: world -> object space (the reference's names)
+    float4 normal[3];           // world hit point -> unnormalised world normal: the affine composite
+                                // MatrixToNormal * (MatrixToWorld * p - centre) / r (Sphere.cs:50-155)
 };
 
 struct alignas(16) MatF {       // per primitive ID, 80 B

@@ -196,13 +196,18 @@ int upload_scene(rt_scene* s)
                 std::memcpy(X.to_normal, p.to_normal, sizeof X.to_normal);
                 xd.push_back(X);
                 XformF F;
+                const double c[3] = {p.center.x, p.center.y, p.center.z};
                 for (int r = 0; r < 3; r++) {
                     F.to_world[r] = make_float4((float)p.to_world[4 * r], (float)p.to_world[4 * r + 1],
                                                 (float)p.to_world[4 * r + 2], (float)p.to_world[4 * r + 3]);
-                    F.to_obj[r] = make_float4((float)p.to_obj[4 * r], (float)p.to_obj[4 * r + 1],
-                                              (float)p.to_obj[4 * r + 2], (float)p.to_obj[4 * r + 3]);
-                    F.to_normal[r] = make_float4((float)p.to_normal[4 * r], (float)p.to_normal[4 * r + 1],
-                                                 (float)p.to_normal[4 * r + 2], (float)p.to_normal[4 * r + 3]);
+                    // normal(p) = N3 * (W * p + w - c) / r: one affine map of the world hit point
+                    double row[4] = {0, 0, 0, 0};
+                    for (int k = 0; k < 3; k++) {
+                        const double nk = p.to_normal[4 * r + k] / p.radius;
+                        for (int j = 0; j < 3; j++) row[j] += nk * p.to_world[4 * k + j];
+                        row[3] += nk * (p.to_world[4 * k + 3] - c[k]);
+                    }
+                    F.normal[r] = make_float4((float)row[0], (float)row[1], (float)row[2], (float)row[3]);
                 }
                 xf.push_back(F);
             }
