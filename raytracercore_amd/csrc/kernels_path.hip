@@ -184,6 +184,46 @@ __device__ __forceinline__ void rect_group(const RectRec* __restrict__ r, int n,
 #endif
 }
 
+// Closed box (BoxRec): one slab test gives the entry and exit distances and faces; each is a
+// hit when it lies in [0, best), its face keeps hits from that side (culling) and it is not the
+// face the ray leaves (self-hit).  The entry wins when both are hits.  Equivalent to testing the
+// six faces as rectangles (a convex box is met at most twice), up to ties on its edges.
+// SUB: oi holds o itself (frame-local rays), as in hit_rect.
+template <bool SUB>
+__device__ __forceinline__ void hit_box(const BoxRec& B, V3 o, V3 d, V3 id, V3 oi, int prev, Best& b)
+{
+    const float lx = SUB ? (B.lo.x - oi.x) * id.x : fmaf(B.lo.x, id.x, -oi.x);
+    const float hx = SUB ? (B.hi.x - oi.x) * id.x : fmaf(B.hi.x, id.x, -oi.x);
+    const float ly = SUB ? (B.lo.y - oi.y) * id.y : fmaf(B.lo.y, id.y, -oi.y);
+    const float hy = SUB ? (B.hi.y - oi.y) * id.y : fmaf(B.hi.y, id.y, -oi.y);
+    const float lz = SUB ? (B.lo.z - oi.z) * id.z : fmaf(B.lo.z, id.z, -oi.z);
+    const float hz = SUB ? (B.hi.z - oi.z) * id.z : fmaf(B.hi.z, id.z, -oi.z);
+    const float nx = fminf(lx, hx), ny = fminf(ly, hy), nz = fminf(lz, hz);
+    const float fx = fmaxf(lx, hx), fy = fmaxf(ly, hy), fz = fmaxf(lz, hz);
+    const float te = fmaxf(fmaxf(nx, ny), nz), tx = fminf(fminf(fx, fy), fz);
+    const bool meet = te <= tx;
+    // the ray enters axis a's slab by its lower plane (side 0) when d[a] > 0
+    const int sx = (int)(__float_as_uint(d.x) >> 31), sy = (int)(__float_as_uint(d.y) >> 31),
+              sz = (int)(__float_as_uint(d.z) >> 31);
+    const uint32_t perm = __float_as_uint(B.hi.w), keep = B.keep;
+    const uint32_t rel_prev = (uint32_t)(prev - __float_as_int(B.lo.w)); // face IDs: id0 + (perm >> 4f & 15)
+    bool ok_e = false, ok_x = false;
+    int fe = 0, fo = 0;
+    if (keep & 0x3Fu) { // some face keeps entry hits (wave-uniform)
+        fe = te == nx ? sx : (te == ny ? 2 + sy : 4 + sz);
+        ok_e = meet & (__float_as_uint(te) < __float_as_uint(b.t)) & (((perm >> (4 * fe)) & 15u) != rel_prev);
+        if ((keep & 0x3Fu) != 0x3Fu) ok_e &= ((keep >> fe) & 1u) != 0;
+    }
+    if (keep & 0x3F00u) { // some face keeps exit hits
+        fo = tx == fx ? 1 - sx : (tx == fy ? 3 - sy : 5 - sz);
+        ok_x = meet & (__float_as_uint(tx) < __float_as_uint(b.t)) & (((perm >> (4 * fo)) & 15u) != rel_prev);
+        if ((keep & 0x3F00u) != 0x3F00u) ok_x &= ((keep >> (8 + fo)) & 1u) != 0;
+    }
+    const bool ok = ok_e | ok_x;
+    b.t = ok ? (ok_e ? te : tx) : b.t;
+    b.sg = ok ? B.sg0 + 2 * (ok_e ? fe : fo) : b.sg;
+}
+
 // 1/d for the box tests, with |d| clamped to >= 2^-64 so that an axis-parallel ray (d = 0 on an
 // axis, e.g. a diffuse bounce whose angle draw is exactly 0) gives large finite slab distances of
 // the right sign instead of 0 * inf = NaN, which the min/max chains would ignore (a box the ray
@@ -224,7 +264,7 @@ __device__ __forceinline__ void trace_brute(const PathScene& s, const GroupRec* 
             if (!__any(slab(G.lo, G.hi, oi, id, b.t, tn))) continue;
         }
         if (STATS) { // primitive tests actually made (groups the wave skipped are not counted)
-            n_flat += G.n_rect[0] + G.n_rect[1] + G.n_rect[2] + G.n_frame_rects + (G.n_tri_sph & 0xFFFF);
+            n_flat += G.n_rect[0] + G.n_rect[1] + G.n_rect[2] + G.n_flat_extra + (G.n_tri_sph & 0xFFFF);
             n_sph += G.n_tri_sph >> 16;
         }
         const RectRec* r = rects + __float_as_int(G.lo.w);
@@ -233,6 +273,9 @@ __device__ __forceinline__ void trace_brute(const PathScene& s, const GroupRec* 
         rect_group<1>(r, G.n_rect[1], o, d, id, oi, prev, b);
         r += G.n_rect[1];
         rect_group<2>(r, G.n_rect[2], o, d, id, oi, prev, b);
+        const BoxRec* boxes = reinterpret_cast<const BoxRec*>(frames); // BoxRecs share the frame array
+        for (int j = G.frame_first + G.n_frames; j < G.frame_first + G.n_frames + G.n_boxes; j++)
+            hit_box<false>(boxes[j], o, d, id, oi, prev, b);
         // rectangles in a common affine frame: the ray mapped once, then the same rect tests (t is
         // invariant under the map; a local d of 0 gives an infinite or NaN t, which never hits)
 #ifndef RT_EXP_NO_FRAMES
@@ -247,6 +290,7 @@ __device__ __forceinline__ void trace_brute(const PathScene& s, const GroupRec* 
             rect_group<1, true>(fr, F.n_rect[1], lo, ld, lid, lo, prev, b);
             fr += F.n_rect[1];
             rect_group<2, true>(fr, F.n_rect[2], lo, ld, lid, lo, prev, b);
+            if (F.box >= 0) hit_box<true>(boxes[F.box], lo, ld, lid, lo, prev, b);
         }
 #endif
         int i = __float_as_int(G.hi.w);

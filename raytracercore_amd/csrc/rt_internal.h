@@ -50,8 +50,24 @@ struct alignas(16) RectRec {
 struct alignas(16) FrameRec {
     float4 r0, r1, r2;          // local = (r_k . p + r_k.w)
     int32_t rect_first;
-    int32_t n_rect[3];
+    int16_t n_rect[3];
+    int16_t box;                // index of the frame's BoxRec in the same array, or -1
 };
+
+// Six rectangles that close an axis-aligned box (in world space, or in a frame) are tested
+// together by one slab test: the candidates are the face the ray enters by and the face it
+// leaves by, each kept under its face's culling rule and self-hit rule, entry first (a convex
+// box is met at most twice).  Faces f = 2 axis + side (side 0 = the lower plane) occupy slots
+// sg0 / 2 + f; their primitive IDs are id0 + (perm >> 4 f & 15).  Stored in the FrameRec array
+// (same 64-B size) so that the kernel needs no further argument.
+struct alignas(16) BoxRec {
+    float4 lo;                  // xyz: lower planes, w = bitcast id0
+    float4 hi;                  // xyz: upper planes, w = bitcast perm
+    uint32_t keep;              // bit f: face f kept as an entry hit, bit 8 + f: as an exit hit
+    int32_t sg0;                // slot of face 0, << 1
+    int32_t pad[6];
+};
+static_assert(sizeof(BoxRec) == sizeof(FrameRec), "boxes share the frame array");
 
 // ---- exact fp64 scene (primary-ID pass) -----------------------------------------------
 struct alignas(16) Vec4d {
@@ -107,16 +123,17 @@ struct alignas(16) MatF {       // per primitive ID, 80 B
 
 // A group of the brute-force slot order (64 B): its primitives' box (fp32, rounded outward) and
 // typed ranges -- world rects (x | y | z) in RectRec order from rect_first, then n_frames
-// FrameRecs from frame_first (their rects follow the world rects), then triangles and spheres in
-// slot order from tri_slot.  The grouped kernel skips a group when no lane of the wave meets its
+// FrameRecs and n_boxes world BoxRecs from frame_first (the frames' rects follow the world rects),
+// then triangles and spheres in slot order from tri_slot.  The grouped kernel skips a group when no lane of the wave meets its
 // box; the flat order is one group whose box is never tested.
 struct alignas(16) GroupRec {
     float4 lo;     // xyz, w = bitcast rect_first
     float4 hi;     // xyz, w = bitcast tri_slot
     int32_t n_rect[3];
     int32_t n_tri_sph; // n_tri | n_sph << 16
-    int32_t frame_first, n_frames;
-    int32_t n_frame_rects; // rect tests of the group's frames (statistics)
+    int32_t frame_first;
+    int16_t n_frames, n_boxes; // FrameRecs, then world BoxRecs, from frame_first
+    int32_t n_flat_extra;      // faces tested through frames and boxes (statistics)
     int32_t pad;
 };
 

@@ -6,6 +6,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -374,46 +375,126 @@ int upload_scene(rt_scene* s)
             M[k][3] = -(M[k][0] * F.org.x + M[k][1] * F.org.y + M[k][2] * F.org.z);
         }
     };
-    auto frame_rect = [&](const FrameB& F, const double M[3][4], int i, int k) {
+    // Rectangle geometry in double (world axes, or a frame's local axes): plane coordinate c on
+    // axis k, extents on the other two axes in increasing axis order, and sign(N . axis k).
+    struct RectG {
+        int i, k;
+        double c, lo1, hi1, lo2, hi2;
+        double ns;
+    };
+    auto rect_geom = [&](int i, int k, const double (*M)[4], const FrameB* F) {
         const HostPrim& p = H[i];
-        auto loc = [&](double x, double y, double z, int a) { return M[a][0] * x + M[a][1] * y + M[a][2] * z + M[a][3]; };
+        auto loc = [&](double x, double y, double z, int a) {
+            if (!M) return a == 0 ? x : a == 1 ? y : z;
+            return M[a][0] * x + M[a][1] * y + M[a][2] * z + M[a][3];
+        };
         const Vec4d v0 = p.v[0], e1 = p.e01, e2 = p.e02;
         const double cx[4] = {v0.x, v0.x + e1.x, v0.x + e2.x, v0.x + e1.x + e2.x};
         const double cy[4] = {v0.y, v0.y + e1.y, v0.y + e2.y, v0.y + e1.y + e2.y};
         const double cz[4] = {v0.z, v0.z + e1.z, v0.z + e2.z, v0.z + e1.z + e2.z};
         const int a1 = k == 0 ? 1 : 0, a2 = k == 2 ? 1 : 2;
-        double c = 0, lo1 = 1e300, hi1 = -1e300, lo2 = 1e300, hi2 = -1e300;
+        RectG g{i, k, 0, 1e300, -1e300, 1e300, -1e300, 0};
         for (int j = 0; j < 4; j++) {
-            c += 0.25 * loc(cx[j], cy[j], cz[j], k);
+            g.c += 0.25 * loc(cx[j], cy[j], cz[j], k);
             const double q1 = loc(cx[j], cy[j], cz[j], a1), q2 = loc(cx[j], cy[j], cz[j], a2);
-            lo1 = std::min(lo1, q1);
-            hi1 = std::max(hi1, q1);
-            lo2 = std::min(lo2, q2);
-            hi2 = std::max(hi2, q2);
+            g.lo1 = std::min(g.lo1, q1);
+            g.hi1 = std::max(g.hi1, q1);
+            g.lo2 = std::min(g.lo2, q2);
+            g.hi2 = std::max(g.hi2, q2);
         }
+        if (!M) g.c = k == 0 ? v0.x : k == 1 ? v0.y : v0.z; // world rects sit exactly on v0's plane
+        const double nk = F ? dot_s(p.n, F->b[k]) : (k == 0 ? p.n.x : k == 1 ? p.n.y : p.n.z);
+        g.ns = nk > 0 ? 1.0 : -1.0;
+        return g;
+    };
+    auto frame_rect = [&](const RectG& g) {
+        const HostPrim& p = H[g.i];
         RectRec r;
-        r.c = (float)c;
-        r.m1 = (float)(0.5 * (lo1 + hi1));
-        r.m2 = (float)(0.5 * (lo2 + hi2));
+        r.c = (float)g.c;
+        r.m1 = (float)(0.5 * (g.lo1 + g.hi1));
+        r.m2 = (float)(0.5 * (g.lo2 + g.hi2));
         // half-widths padded by 2^-21 relative: the fp32 frame rows move the shared edges of
         // neighbouring faces by about an ulp, and a padded edge is met by both faces (closest wins)
-        r.h1 = (float)(0.5 * (hi1 - lo1) + (std::fabs(0.5 * (lo1 + hi1)) + 0.5 * (hi1 - lo1)) * 4.76837158203125e-07);
-        r.h2 = (float)(0.5 * (hi2 - lo2) + (std::fabs(0.5 * (lo2 + hi2)) + 0.5 * (hi2 - lo2)) * 4.76837158203125e-07);
+        r.h1 = (float)(0.5 * (g.hi1 - g.lo1) + (std::fabs(0.5 * (g.lo1 + g.hi1)) + 0.5 * (g.hi1 - g.lo1)) * 4.76837158203125e-07);
+        r.h2 = (float)(0.5 * (g.hi2 - g.lo2) + (std::fabs(0.5 * (g.lo2 + g.hi2)) + 0.5 * (g.hi2 - g.lo2)) * 4.76837158203125e-07);
         // gin = N . d > 0 = sign(N . b_k) * d_local[k] > 0; the culling factor as for world rects
-        const float ns = dot_s(p.n, F.b[k]) > 0 ? 1.0f : -1.0f;
-        r.cull = (p.flags & F_TWOSIDED) ? 0.0f : ((p.flags & F_INVERT) ? -ns : ns);
-        r.id = i;
+        r.cull = (p.flags & F_TWOSIDED) ? 0.0f : ((p.flags & F_INVERT) ? -(float)g.ns : (float)g.ns);
+        r.id = g.i;
         r.sg = 0;
         return r;
     };
-    // Brute-force slot orders: groups of primitives, each [x-rects | y-rects | z-rects | frame
-    // rects | triangles | spheres], then the planes.  The flat order is one group of everything;
-    // the grouped order cuts the SAH BVH into subtrees of at most kGroupMax primitives.
+    // Closed boxes: six of the rectangles, two per axis at distinct planes, whose extents are the
+    // box's (within 1e-9 relative), with primitive IDs within 16 of each other.  Returns face
+    // lists in face order f = 2 axis + side.
+    auto find_boxes = [&](const std::vector<RectG>& rg, std::vector<char>& used) {
+        std::vector<std::array<int, 6>> boxes;
+        auto eq = [](double a, double b, double sc) { return std::fabs(a - b) <= 1e-9 * sc; };
+        for (size_t A = 0; A < rg.size(); A++) {
+            if (used[A] || rg[A].k != 0) continue;
+            for (size_t B = 0; B < rg.size(); B++) {
+                if (B == A || used[B] || used[A] || rg[B].k != 0) continue;
+                const RectG &ga = rg[A], &gb = rg[B];
+                const double x0 = std::min(ga.c, gb.c), x1 = std::max(ga.c, gb.c);
+                const double y0 = ga.lo1, y1 = ga.hi1, z0 = ga.lo2, z1 = ga.hi2;
+                const double sc = std::max({std::fabs(x0), std::fabs(x1), std::fabs(y0), std::fabs(y1), std::fabs(z0),
+                                            std::fabs(z1), x1 - x0, y1 - y0, z1 - z0});
+                if (!(x1 - x0 > 1e-9 * sc) || !(y1 - y0 > 1e-9 * sc) || !(z1 - z0 > 1e-9 * sc)) continue;
+                if (!eq(gb.lo1, y0, sc) || !eq(gb.hi1, y1, sc) || !eq(gb.lo2, z0, sc) || !eq(gb.hi2, z1, sc)) continue;
+                // the face with extents (e1lo, e1hi, e2lo, e2hi) on plane c of axis k
+                auto find = [&](int k, double c, double l1, double h1, double l2, double h2) {
+                    for (size_t j = 0; j < rg.size(); j++)
+                        if (!used[j] && rg[j].k == k && eq(rg[j].c, c, sc) && eq(rg[j].lo1, l1, sc) &&
+                            eq(rg[j].hi1, h1, sc) && eq(rg[j].lo2, l2, sc) && eq(rg[j].hi2, h2, sc))
+                            return (int)j;
+                    return -1;
+                };
+                const int fy0 = find(1, y0, x0, x1, z0, z1), fy1 = find(1, y1, x0, x1, z0, z1);
+                const int fz0 = find(2, z0, x0, x1, y0, y1), fz1 = find(2, z1, x0, x1, y0, y1);
+                if (fy0 < 0 || fy1 < 0 || fz0 < 0 || fz1 < 0) continue;
+                const std::array<int, 6> f = {ga.c < gb.c ? (int)A : (int)B, ga.c < gb.c ? (int)B : (int)A, fy0, fy1, fz0, fz1};
+                int idmin = 1 << 30, idmax = -1;
+                for (int j : f) {
+                    idmin = std::min(idmin, rg[j].i);
+                    idmax = std::max(idmax, rg[j].i);
+                }
+                if (idmax - idmin >= 16) continue;
+                for (int j : f) used[j] = 1;
+                boxes.push_back(f);
+            }
+        }
+        return boxes;
+    };
+    auto box_rec = [&](const std::vector<RectG>& rg, const std::array<int, 6>& f, int slot0) {
+        BoxRec B;
+        std::memset(&B, 0, sizeof B);
+        int id0 = 1 << 30;
+        for (int j : f) id0 = std::min(id0, rg[j].i);
+        uint32_t perm = 0, keep = 0;
+        for (int fi = 0; fi < 6; fi++) {
+            const RectG& g = rg[f[fi]];
+            const uint32_t fl = H[g.i].flags;
+            perm |= (uint32_t)(g.i - id0) << (4 * fi);
+            // entering through the lower plane moves along +axis: Inside (N . d > 0) iff sign(N_k) > 0
+            const bool gin_entry = (fi & 1) == 0 ? g.ns > 0 : g.ns < 0;
+            const bool two = (fl & F_TWOSIDED) != 0, inv = (fl & F_INVERT) != 0;
+            if (two || gin_entry == inv) keep |= 1u << fi;
+            if (two || !gin_entry == inv) keep |= 1u << (8 + fi);
+        }
+        B.lo = make_float4((float)rg[f[0]].c, (float)rg[f[2]].c, (float)rg[f[4]].c, as_f(id0));
+        B.hi = make_float4((float)rg[f[1]].c, (float)rg[f[3]].c, (float)rg[f[5]].c, as_f(perm));
+        B.keep = keep;
+        B.sg0 = slot0 << 1;
+        return B;
+    };
+    // Brute-force slot orders: groups of primitives, each [x-rects | y-rects | z-rects | world
+    // box faces | frame rects and frame box faces | triangles | spheres], then the planes.  The
+    // flat order is one group of everything; the grouped order cuts the SAH BVH into subtrees of
+    // at most kGroupMax primitives.
     struct BruteOrder {
         std::vector<PrimF> prims;
         std::vector<TestRec> tests;
         std::vector<RectRec> rects;
-        std::vector<FrameRec> frames;
+        std::vector<FrameRec> frames; // FrameRecs and BoxRecs
         std::vector<GroupRec> groups;
         int nr[3] = {0, 0, 0}, nt = 0, ns = 0;
     };
@@ -432,6 +513,7 @@ int upload_scene(rt_scene* s)
             }
         }
     };
+    const bool use_boxes = !getenv("RTCORE_NO_BOXES"); // A/B switch for measurements
     auto build_order = [&](const std::vector<std::vector<int>>& groups) {
         BruteOrder o;
         for (const auto& g : groups) {
@@ -441,62 +523,117 @@ int upload_scene(rt_scene* s)
             fbox(g, lo, hi);
             const int rect_first = (int)o.rects.size();
             int cnt[5] = {0, 0, 0, 0, 0};
-            int tri_slot = 0;
+            auto push_slot = [&](int i, PrimF f) {
+                o.prims.push_back(f);
+                o.tests.push_back(testrec(i));
+            };
+            // world rects: closed boxes first, the rest as single rects
+            std::vector<RectG> wr;
+            for (int i : g)
+                if (kind_of[i] < 3) wr.push_back(rect_geom(i, kind_of[i], nullptr, nullptr));
+            std::vector<char> wused(wr.size(), 0);
+            const auto wboxes = use_boxes ? find_boxes(wr, wused) : std::vector<std::array<int, 6>>{};
+            for (int kind = 0; kind < 3; kind++)
+                for (size_t j = 0; j < wr.size(); j++) {
+                    if (wused[j] || wr[j].k != kind) continue;
+                    const int i = wr[j].i;
+                    PrimF f = primf(i);
+                    const uint32_t fl = p_flags_with_axis(H[i].flags, kind);
+                    std::memcpy(&f.b.w, &fl, 4);
+                    o.rects.push_back(rectrec(i, kind));
+                    o.rects.back().sg = (int)o.prims.size() << 1;
+                    o.nr[kind]++;
+                    cnt[kind]++;
+                    push_slot(i, f);
+                }
+            // frames (their rects after the world rects), then the world boxes, in one array
             const std::vector<FrameB> frames = find_frames(g);
             std::vector<char> in_frame(n, 0);
             for (const auto& F : frames)
                 for (int k = 0; k < 3; k++)
                     for (int i : F.face[k]) in_frame[i] = 1;
-            auto push_slot = [&](int i, PrimF f) {
-                o.prims.push_back(f);
-                o.tests.push_back(testrec(i));
-            };
-            for (int kind = 0; kind < 5; kind++) {
-                if (kind == 3) { // the frames' rects, then the remaining triangles
-                    G.frame_first = (int)o.frames.size();
-                    G.n_frames = (int)frames.size();
-                    for (const auto& F : frames) {
-                        double M[3][4];
-                        frame_rows(F, M);
-                        FrameRec R;
-                        std::memset(&R, 0, sizeof R);
-                        float4* rows[3] = {&R.r0, &R.r1, &R.r2};
-                        for (int k = 0; k < 3; k++)
-                            *rows[k] = make_float4((float)M[k][0], (float)M[k][1], (float)M[k][2], (float)M[k][3]);
-                        R.rect_first = (int)o.rects.size();
-                        for (int k = 0; k < 3; k++) {
-                            R.n_rect[k] = (int)F.face[k].size();
-                            for (int i : F.face[k]) {
-                                o.rects.push_back(frame_rect(F, M, i, k));
-                                o.rects.back().sg = (int)o.prims.size() << 1;
-                                PrimF f = primf(i);
-                                const uint32_t fl = H[i].flags | F_FRAME_RECT;
-                                std::memcpy(&f.b.w, &fl, 4);
-                                push_slot(i, f);
-                                G.n_frame_rects++;
-                                o.nt++;
-                            }
-                        }
-                        o.frames.push_back(R);
+            G.frame_first = (int)o.frames.size();
+            G.n_frames = (int16_t)frames.size();
+            G.n_boxes = (int16_t)wboxes.size();
+            std::vector<BoxRec> frame_boxes;
+            const int frame_box_first = G.frame_first + (int)frames.size() + (int)wboxes.size();
+            for (const auto& F : frames) {
+                double M[3][4];
+                frame_rows(F, M);
+                FrameRec R;
+                std::memset(&R, 0, sizeof R);
+                float4* rows[3] = {&R.r0, &R.r1, &R.r2};
+                for (int k = 0; k < 3; k++)
+                    *rows[k] = make_float4((float)M[k][0], (float)M[k][1], (float)M[k][2], (float)M[k][3]);
+                std::vector<RectG> fr;
+                for (int k = 0; k < 3; k++)
+                    for (int i : F.face[k]) fr.push_back(rect_geom(i, k, M, &F));
+                std::vector<char> fused(fr.size(), 0);
+                auto fb = use_boxes ? find_boxes(fr, fused) : std::vector<std::array<int, 6>>{};
+                for (size_t bi = 1; bi < fb.size(); bi++) // one box per frame; further ones stay rects
+                    for (int fi = 0; fi < 6; fi++) fused[fb[bi][fi]] = 0;
+                fb.resize(std::min<size_t>(fb.size(), 1));
+                R.rect_first = (int)o.rects.size();
+                for (int k = 0; k < 3; k++) {
+                    R.n_rect[k] = 0;
+                    for (size_t j = 0; j < fr.size(); j++) {
+                        if (fused[j] || fr[j].k != k) continue;
+                        const int i = fr[j].i;
+                        o.rects.push_back(frame_rect(fr[j]));
+                        o.rects.back().sg = (int)o.prims.size() << 1;
+                        PrimF f = primf(i);
+                        const uint32_t fl = H[i].flags | F_FRAME_RECT;
+                        std::memcpy(&f.b.w, &fl, 4);
+                        push_slot(i, f);
+                        R.n_rect[k]++;
+                        G.n_flat_extra++;
+                        o.nt++;
                     }
-                    tri_slot = (int)o.prims.size();
                 }
+                R.box = -1;
+                if (!fb.empty()) { // at most one closed box per frame is tested as a box
+                    R.box = (int16_t)(frame_box_first + (int)frame_boxes.size());
+                    frame_boxes.push_back(box_rec(fr, fb[0], (int)o.prims.size()));
+                    for (int fi = 0; fi < 6; fi++) {
+                        const int i = fr[fb[0][fi]].i;
+                        PrimF f = primf(i);
+                        const uint32_t fl = H[i].flags | F_FRAME_RECT;
+                        std::memcpy(&f.b.w, &fl, 4);
+                        push_slot(i, f);
+                        G.n_flat_extra++;
+                        o.nt++;
+                    }
+                }
+                o.frames.push_back(R);
+            }
+            for (const auto& f6 : wboxes) {
+                BoxRec B = box_rec(wr, f6, (int)o.prims.size());
+                for (int fi = 0; fi < 6; fi++) {
+                    const int i = wr[f6[fi]].i, kind = fi >> 1;
+                    PrimF f = primf(i);
+                    const uint32_t fl = p_flags_with_axis(H[i].flags, kind);
+                    std::memcpy(&f.b.w, &fl, 4);
+                    push_slot(i, f);
+                    G.n_flat_extra++;
+                    o.nr[kind]++;
+                }
+                FrameRec R;
+                std::memcpy(&R, &B, sizeof R);
+                o.frames.push_back(R);
+            }
+            for (const auto& B : frame_boxes) {
+                FrameRec R;
+                std::memcpy(&R, &B, sizeof R);
+                o.frames.push_back(R);
+            }
+            const int tri_slot = (int)o.prims.size();
+            for (int kind = 3; kind < 5; kind++)
                 for (int i : g) {
                     if (kind_of[i] != kind || (kind == 3 && in_frame[i])) continue;
-                    PrimF f = primf(i);
-                    if (kind < 3) {
-                        const uint32_t fl = p_flags_with_axis(H[i].flags, kind);
-                        std::memcpy(&f.b.w, &fl, 4);
-                        o.rects.push_back(rectrec(i, kind));
-                        o.rects.back().sg = (int)o.prims.size() << 1;
-                        o.nr[kind]++;
-                    } else {
-                        (kind == 3 ? o.nt : o.ns)++;
-                    }
+                    (kind == 3 ? o.nt : o.ns)++;
                     cnt[kind]++;
-                    push_slot(i, f);
+                    push_slot(i, primf(i));
                 }
-            }
             G.lo = make_float4(lo[0], lo[1], lo[2], as_f(rect_first));
             G.hi = make_float4(hi[0], hi[1], hi[2], as_f(tri_slot));
             for (int k = 0; k < 3; k++) G.n_rect[k] = cnt[k];
