@@ -1148,7 +1148,7 @@ PathScene make_path_scene(const DevScene& s)
     ps.n_tri = s.n_tri;
     ps.n_sph = s.n_sph;
     ps.n_pln = s.n_pln;
-    ps.n_bvh = s.n_rect[0] + s.n_rect[1] + s.n_rect[2] + s.n_tri + s.n_sph;
+    ps.n_bvh = s.pln0_bf; // set per order by launch_path
     ps.n_slots = ps.n_bvh + s.n_pln;
     ps.n_ids = s.n_ids;
     ps.n_xf = s.n_xf;
@@ -1170,7 +1170,7 @@ int path_wide_stack() { return RT_WIDE_STACK; }
 
 size_t path_lds_bytes(const DevScene& s)
 {
-    const size_t slots = (size_t)s.n_rect[0] + s.n_rect[1] + s.n_rect[2] + s.n_tri + s.n_sph + s.n_pln;
+    const size_t slots = (size_t)std::max(std::max(s.pln0_bf, s.pln0_gr), s.pln0_bvh) + s.n_pln;
     return slots * sizeof(PrimF) + (size_t)s.n_ids * sizeof(MatF) + (size_t)s.n_xf * sizeof(XformF);
 }
 
@@ -1194,6 +1194,8 @@ hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams
     if (kernel == 3) ps.root = s.root4; // the wide kernel walks the collapsed tree
     const bool grouped = kernel == 1, bvh = kernel >= 2;
     ps.n_groups = grouped ? s.n_groups_gr : 1;
+    ps.n_bvh = bvh ? s.pln0_bvh : grouped ? s.pln0_gr : s.pln0_bf;
+    ps.n_slots = ps.n_bvh + s.n_pln;
     const CameraF* ca = d_cam;
     PathParams pa = p;
     const TestRec* tests = bvh ? s.tests_bvh : grouped ? s.tests_gr : s.tests_bf;

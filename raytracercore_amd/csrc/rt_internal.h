@@ -276,7 +276,8 @@ struct DevScene {
     const GroupRec* groups_gr;
     int32_t n_groups_gr;
     int32_t n_rect[3];
-    int32_t n_tri, n_sph, n_pln; // n_tri counts general triangles (frame rects included), not world rects
+    int32_t n_tri, n_sph, n_pln; // flat-order slots: n_tri counts general triangles (frame rects included)
+    int32_t pln0_bf, pln0_gr, pln0_bvh; // first plane slot of the flat, grouped and BVH orders
     const TestRec* tests_bvh;
     const PrimF* prims_bvh;
     const NodeF* nodes;

@@ -423,55 +423,86 @@ int upload_scene(rt_scene* s)
         r.sg = 0;
         return r;
     };
-    // Closed boxes: six of the rectangles, two per axis at distinct planes, whose extents are the
-    // box's (within 1e-9 relative), with primitive IDs within 16 of each other.  Returns face
-    // lists in face order f = 2 axis + side.
+    // Boxes: rectangles on the faces of one axis-aligned box -- a pair on some axis with equal
+    // extents, and the other faces on the planes and extents of the box they span (within 1e-9
+    // relative), at least five of the six, with primitive IDs within 16 of each other.  Face
+    // lists are in face order f = 2 axis + side, -1 for a missing face (an open box: the ray may
+    // enter through the opening, and its exit face is still the other candidate).
+    struct BoxFit {
+        std::array<int, 6> f;
+        double lo[3], hi[3];
+    };
     auto find_boxes = [&](const std::vector<RectG>& rg, std::vector<char>& used) {
-        std::vector<std::array<int, 6>> boxes;
+        std::vector<BoxFit> boxes;
         auto eq = [](double a, double b, double sc) { return std::fabs(a - b) <= 1e-9 * sc; };
-        for (size_t A = 0; A < rg.size(); A++) {
-            if (used[A] || rg[A].k != 0) continue;
-            for (size_t B = 0; B < rg.size(); B++) {
-                if (B == A || used[B] || used[A] || rg[B].k != 0) continue;
-                const RectG &ga = rg[A], &gb = rg[B];
-                const double x0 = std::min(ga.c, gb.c), x1 = std::max(ga.c, gb.c);
-                const double y0 = ga.lo1, y1 = ga.hi1, z0 = ga.lo2, z1 = ga.hi2;
-                const double sc = std::max({std::fabs(x0), std::fabs(x1), std::fabs(y0), std::fabs(y1), std::fabs(z0),
-                                            std::fabs(z1), x1 - x0, y1 - y0, z1 - z0});
-                if (!(x1 - x0 > 1e-9 * sc) || !(y1 - y0 > 1e-9 * sc) || !(z1 - z0 > 1e-9 * sc)) continue;
-                if (!eq(gb.lo1, y0, sc) || !eq(gb.hi1, y1, sc) || !eq(gb.lo2, z0, sc) || !eq(gb.hi2, z1, sc)) continue;
-                // the face with extents (e1lo, e1hi, e2lo, e2hi) on plane c of axis k
-                auto find = [&](int k, double c, double l1, double h1, double l2, double h2) {
-                    for (size_t j = 0; j < rg.size(); j++)
-                        if (!used[j] && rg[j].k == k && eq(rg[j].c, c, sc) && eq(rg[j].lo1, l1, sc) &&
-                            eq(rg[j].hi1, h1, sc) && eq(rg[j].lo2, l2, sc) && eq(rg[j].hi2, h2, sc))
-                            return (int)j;
-                    return -1;
-                };
-                const int fy0 = find(1, y0, x0, x1, z0, z1), fy1 = find(1, y1, x0, x1, z0, z1);
-                const int fz0 = find(2, z0, x0, x1, y0, y1), fz1 = find(2, z1, x0, x1, y0, y1);
-                if (fy0 < 0 || fy1 < 0 || fz0 < 0 || fz1 < 0) continue;
-                const std::array<int, 6> f = {ga.c < gb.c ? (int)A : (int)B, ga.c < gb.c ? (int)B : (int)A, fy0, fy1, fz0, fz1};
-                int idmin = 1 << 30, idmax = -1;
-                for (int j : f) {
-                    idmin = std::min(idmin, rg[j].i);
-                    idmax = std::max(idmax, rg[j].i);
+        for (int pa = 0; pa < 3; pa++)
+            for (size_t A = 0; A < rg.size(); A++) {
+                if (used[A] || rg[A].k != pa) continue;
+                for (size_t B = 0; B < rg.size(); B++) {
+                    if (B == A || used[B] || used[A] || rg[B].k != pa) continue;
+                    const RectG &ga = rg[A], &gb = rg[B];
+                    // the pair's axis pa and its two in-plane axes (increasing order)
+                    const int q1 = pa == 0 ? 1 : 0, q2 = pa == 2 ? 1 : 2;
+                    double lo[3], hi[3];
+                    lo[pa] = std::min(ga.c, gb.c);
+                    hi[pa] = std::max(ga.c, gb.c);
+                    lo[q1] = ga.lo1;
+                    hi[q1] = ga.hi1;
+                    lo[q2] = ga.lo2;
+                    hi[q2] = ga.hi2;
+                    double sc = 0;
+                    for (int k = 0; k < 3; k++) sc = std::max({sc, std::fabs(lo[k]), std::fabs(hi[k]), hi[k] - lo[k]});
+                    bool flat = false;
+                    for (int k = 0; k < 3; k++) flat |= !(hi[k] - lo[k] > 1e-9 * sc);
+                    if (flat || !eq(gb.lo1, ga.lo1, sc) || !eq(gb.hi1, ga.hi1, sc) || !eq(gb.lo2, ga.lo2, sc) ||
+                        !eq(gb.hi2, ga.hi2, sc))
+                        continue;
+                    BoxFit fit;
+                    fit.f.fill(-1);
+                    fit.f[2 * pa] = ga.c < gb.c ? (int)A : (int)B;
+                    fit.f[2 * pa + 1] = ga.c < gb.c ? (int)B : (int)A;
+                    int found = 2;
+                    for (int k = 0; k < 3; k++) {
+                        fit.lo[k] = lo[k];
+                        fit.hi[k] = hi[k];
+                        if (k == pa) continue;
+                        const int a1 = k == 0 ? 1 : 0, a2 = k == 2 ? 1 : 2;
+                        for (int side = 0; side < 2; side++) {
+                            const double c = side ? hi[k] : lo[k];
+                            for (size_t j = 0; j < rg.size(); j++)
+                                if (!used[j] && rg[j].k == k && eq(rg[j].c, c, sc) && eq(rg[j].lo1, lo[a1], sc) &&
+                                    eq(rg[j].hi1, hi[a1], sc) && eq(rg[j].lo2, lo[a2], sc) && eq(rg[j].hi2, hi[a2], sc)) {
+                                    fit.f[2 * k + side] = (int)j;
+                                    found++;
+                                    break;
+                                }
+                        }
+                    }
+                    if (found < 5) continue;
+                    int idmin = 1 << 30, idmax = -1;
+                    for (int j : fit.f)
+                        if (j >= 0) {
+                            idmin = std::min(idmin, rg[j].i);
+                            idmax = std::max(idmax, rg[j].i);
+                        }
+                    if (idmax - idmin >= 16) continue;
+                    for (int j : fit.f)
+                        if (j >= 0) used[j] = 1;
+                    boxes.push_back(fit);
                 }
-                if (idmax - idmin >= 16) continue;
-                for (int j : f) used[j] = 1;
-                boxes.push_back(f);
             }
-        }
         return boxes;
     };
-    auto box_rec = [&](const std::vector<RectG>& rg, const std::array<int, 6>& f, int slot0) {
+    auto box_rec = [&](const std::vector<RectG>& rg, const BoxFit& fit, int slot0) {
         BoxRec B;
         std::memset(&B, 0, sizeof B);
         int id0 = 1 << 30;
-        for (int j : f) id0 = std::min(id0, rg[j].i);
+        for (int j : fit.f)
+            if (j >= 0) id0 = std::min(id0, rg[j].i);
         uint32_t perm = 0, keep = 0;
         for (int fi = 0; fi < 6; fi++) {
-            const RectG& g = rg[f[fi]];
+            if (fit.f[fi] < 0) continue; // missing face: keeps nothing
+            const RectG& g = rg[fit.f[fi]];
             const uint32_t fl = H[g.i].flags;
             perm |= (uint32_t)(g.i - id0) << (4 * fi);
             // entering through the lower plane moves along +axis: Inside (N . d > 0) iff sign(N_k) > 0
@@ -480,11 +511,20 @@ int upload_scene(rt_scene* s)
             if (two || gin_entry == inv) keep |= 1u << fi;
             if (two || !gin_entry == inv) keep |= 1u << (8 + fi);
         }
-        B.lo = make_float4((float)rg[f[0]].c, (float)rg[f[2]].c, (float)rg[f[4]].c, as_f(id0));
-        B.hi = make_float4((float)rg[f[1]].c, (float)rg[f[3]].c, (float)rg[f[5]].c, as_f(perm));
+        // the planes: a face's own (fp32) coordinate where it exists (hit points are snapped to it)
+        float pl[6];
+        for (int fi = 0; fi < 6; fi++)
+            pl[fi] = (float)(fit.f[fi] >= 0 ? rg[fit.f[fi]].c : ((fi & 1) ? fit.hi[fi >> 1] : fit.lo[fi >> 1]));
+        B.lo = make_float4(pl[0], pl[2], pl[4], as_f(id0));
+        B.hi = make_float4(pl[1], pl[3], pl[5], as_f(perm));
         B.keep = keep;
         B.sg0 = slot0 << 1;
         return B;
+    };
+    // the six slots of a box, face order; a missing face gets a placeholder slot (never hit)
+    auto box_face_prim = [&](const std::vector<RectG>& rg, const BoxFit& fit, int fi) {
+        const int j = fit.f[fi] >= 0 ? fit.f[fi] : fit.f[fi ^ 1] >= 0 ? fit.f[fi ^ 1] : fit.f[(fi + 2) % 6];
+        return rg[j].i;
     };
     // Brute-force slot orders: groups of primitives, each [x-rects | y-rects | z-rects | world
     // box faces | frame rects and frame box faces | triangles | spheres], then the planes.  The
@@ -532,7 +572,7 @@ int upload_scene(rt_scene* s)
             for (int i : g)
                 if (kind_of[i] < 3) wr.push_back(rect_geom(i, kind_of[i], nullptr, nullptr));
             std::vector<char> wused(wr.size(), 0);
-            const auto wboxes = use_boxes ? find_boxes(wr, wused) : std::vector<std::array<int, 6>>{};
+            const auto wboxes = use_boxes ? find_boxes(wr, wused) : std::vector<BoxFit>{};
             for (int kind = 0; kind < 3; kind++)
                 for (size_t j = 0; j < wr.size(); j++) {
                     if (wused[j] || wr[j].k != kind) continue;
@@ -569,9 +609,10 @@ int upload_scene(rt_scene* s)
                 for (int k = 0; k < 3; k++)
                     for (int i : F.face[k]) fr.push_back(rect_geom(i, k, M, &F));
                 std::vector<char> fused(fr.size(), 0);
-                auto fb = use_boxes ? find_boxes(fr, fused) : std::vector<std::array<int, 6>>{};
+                auto fb = use_boxes ? find_boxes(fr, fused) : std::vector<BoxFit>{};
                 for (size_t bi = 1; bi < fb.size(); bi++) // one box per frame; further ones stay rects
-                    for (int fi = 0; fi < 6; fi++) fused[fb[bi][fi]] = 0;
+                    for (int fi = 0; fi < 6; fi++)
+                        if (fb[bi].f[fi] >= 0) fused[fb[bi].f[fi]] = 0;
                 fb.resize(std::min<size_t>(fb.size(), 1));
                 R.rect_first = (int)o.rects.size();
                 for (int k = 0; k < 3; k++) {
@@ -595,12 +636,12 @@ int upload_scene(rt_scene* s)
                     R.box = (int16_t)(frame_box_first + (int)frame_boxes.size());
                     frame_boxes.push_back(box_rec(fr, fb[0], (int)o.prims.size()));
                     for (int fi = 0; fi < 6; fi++) {
-                        const int i = fr[fb[0][fi]].i;
+                        const int i = box_face_prim(fr, fb[0], fi);
                         PrimF f = primf(i);
                         const uint32_t fl = H[i].flags | F_FRAME_RECT;
                         std::memcpy(&f.b.w, &fl, 4);
                         push_slot(i, f);
-                        G.n_flat_extra++;
+                        G.n_flat_extra += fb[0].f[fi] >= 0;
                         o.nt++;
                     }
                 }
@@ -609,12 +650,12 @@ int upload_scene(rt_scene* s)
             for (const auto& f6 : wboxes) {
                 BoxRec B = box_rec(wr, f6, (int)o.prims.size());
                 for (int fi = 0; fi < 6; fi++) {
-                    const int i = wr[f6[fi]].i, kind = fi >> 1;
+                    const int i = box_face_prim(wr, f6, fi), kind = fi >> 1;
                     PrimF f = primf(i);
                     const uint32_t fl = p_flags_with_axis(H[i].flags, kind);
                     std::memcpy(&f.b.w, &fl, 4);
                     push_slot(i, f);
-                    G.n_flat_extra++;
+                    G.n_flat_extra += f6.f[fi] >= 0;
                     o.nr[kind]++;
                 }
                 FrameRec R;
@@ -787,6 +828,10 @@ int upload_scene(rt_scene* s)
     d.prims_gr = s->prims_gr.p;
     d.groups_gr = s->groups_gr.p;
     d.n_groups_gr = (int)grouped.groups.size();
+    // slots before the planes, per order (open boxes add placeholder slots to the brute orders)
+    d.pln0_bf = (int)flat.prims.size() - np;
+    d.pln0_gr = grouped.prims.empty() ? 0 : (int)grouped.prims.size() - np;
+    d.pln0_bvh = n - np;
     for (int k = 0; k < 3; k++) d.n_rect[k] = nr[k];
     d.n_tri = nt;
     d.n_sph = ns;
@@ -837,7 +882,7 @@ int resolve_traversal(rt_scene* s)
 {
     int t = s->traversal;
     if (t == RT_TRAVERSAL_AUTO) {
-        const int n_bvh = s->dev.n_rect[0] + s->dev.n_rect[1] + s->dev.n_rect[2] + s->dev.n_tri + s->dev.n_sph;
+        const int n_bvh = s->dev.pln0_bvh; // primitives other than planes
         t = n_bvh <= 48 ? RT_TRAVERSAL_BRUTE : RT_TRAVERSAL_BVH;
     }
     if (s->traversal == RT_TRAVERSAL_AUTO && t == RT_TRAVERSAL_BRUTE && s->grouped_measured > 1.25)
@@ -886,7 +931,7 @@ int calibrate_grouping(rt_scene* s)
 {
     s->grouped_measured = 0;
     if (s->traversal != RT_TRAVERSAL_AUTO || s->dev.n_groups_gr < 2) return RT_OK;
-    const int n_bvh = s->dev.n_rect[0] + s->dev.n_rect[1] + s->dev.n_rect[2] + s->dev.n_tri + s->dev.n_sph;
+    const int n_bvh = s->dev.pln0_bvh; // primitives other than planes
     if (n_bvh > 48) return RT_OK;
     const int w = std::min(64, s->params.width), h = std::min(64, s->params.height);
     const int x0 = (s->params.width - w) / 2, y0 = (s->params.height - h) / 2;
