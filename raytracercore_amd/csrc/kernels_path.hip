@@ -53,9 +53,8 @@ __device__ __forceinline__ V3 xf_point(const float4* m, V3 p) { return {dot4(m[0
 __device__ __forceinline__ V3 xf_dir(const float4* m, V3 p) { return {dot3(m[0], p), dot3(m[1], p), dot3(m[2], p)}; }
 
 struct Best {
-    float t;    // world distance (Hit.Distance)
-    int sg;     // slot << 1 | geometric inside (before Invert; selects the flipped normal); -1 = none
-    float u, v; // triangle barycentrics | sphere: object-space ray parameter in u | plane: t in u
+    float t; // world distance (Hit.Distance)
+    int sg;  // slot << 1 | geometric inside (before Invert; selects the flipped normal); -1 = none
 };
 __device__ __forceinline__ int pack_sg(int slot, bool gin) { return (slot << 1) | (int)gin; }
 
@@ -75,8 +74,6 @@ __device__ __forceinline__ void hit_tri(const TestRec& R, int slot, V3 o, V3 d, 
     if (!(fl & F_TWOSIDED)) ok &= !(gin ^ ((fl & F_INVERT) != 0)); // one-sided: cull Inside
     b.t = ok ? t : b.t;
     b.sg = ok ? pack_sg(slot, gin) : b.sg;
-    b.u = ok ? u : b.u;
-    b.v = ok ? v : b.v;
 }
 
 // Sphere (Sphere.cs:50-155).  Primitive.RayTrace returns the first surviving root: the close
@@ -113,7 +110,6 @@ __device__ __forceinline__ void hit_sph(const TestRec& R, int slot, V3 o, V3 d, 
     const bool ok = (use_close | use_far) & (tw < b.t);
     b.t = ok ? tw : b.t;
     b.sg = ok ? pack_sg(slot, use_far) : b.sg;
-    b.u = ok ? tc : b.u;
 }
 
 // Plane (Plane.cs:36-66), including the NearlyEqual branch for rays in the plane.
@@ -133,7 +129,6 @@ __device__ __forceinline__ void hit_plane(const TestRec& R, int slot, V3 o, V3 d
     if (!(fl & F_TWOSIDED)) ok &= !(gin ^ ((fl & F_INVERT) != 0));
     b.t = ok ? dist : b.t;
     b.sg = ok ? pack_sg(slot, gin) : b.sg;
-    b.u = ok ? (flat ? 0.0f : t) : b.u;
 }
 
 // Axis-aligned rectangle on plane `AXIS` (RectRec): the same hit as the Mirror parallelogram
@@ -534,7 +529,8 @@ __device__ __forceinline__ float one_minus_exp2_2a(float a)
 // One bounce of Raytracer.GetColor after the closest-hit query.  Returns 0 to continue the
 // path, 1 if the sample ended with colour `col`, 2 if it ended as a miss (Placeholder).
 __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict__ prims, const MatF* __restrict__ mats,
-                                     const XformF* __restrict__ xfs, const float4* __restrict__ vnormals, const Best& b,
+                                     const XformF* __restrict__ xfs, const float4* __restrict__ vnormals,
+                                     const TestRec* __restrict__ tests, const Best& b,
                                      Sample& S, V3& col)
 {
     if (b.sg < 0) {
@@ -573,7 +569,9 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
             n = normalize(xf_point(xfs[__float_as_int(P.b.z)].normal, pos));
         } else { // Triangle.GetNormal quirk: Normal is never set -> NaN when inside
             const float4* vn = vnormals + 3 * id;
-            n = normalize(madd(xyz(vn[2]), b.u + b.v, madd(xyz(vn[1]), b.v, xyz(vn[0]) * b.u)));
+            const TestRec& R = tests[b.sg >> 1]; // barycentrics (u, v) = rows 0, 1 of M (p, 1)
+            const float u = dot4(R.r0, pos), v = dot4(R.r1, pos);
+            n = normalize(madd(xyz(vn[2]), u + v, madd(xyz(vn[1]), v, xyz(vn[0]) * u)));
             if (gin) n = v3(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
         }
     }
@@ -699,7 +697,7 @@ struct Lane {
     int fx, fy, s_next, s_end;
     rt_key2 pkey; // rt_rng_pixel_key of the open item's pixel
     float ar, ag, ab;
-    unsigned n_s, n_m, rays;
+    unsigned n_s, n_m;
     unsigned pool_next, pool_end;
 };
 
@@ -711,7 +709,7 @@ __device__ __forceinline__ void lane_init(Lane& L)
     L.fx = L.fy = L.s_next = L.s_end = 0;
     L.pkey = rt_key2{0u, 0u};
     L.ar = L.ag = L.ab = 0.0f;
-    L.n_s = L.n_m = L.rays = 0;
+    L.n_s = L.n_m = 0;
     L.pool_next = L.pool_end = 0;
 }
 
@@ -776,11 +774,10 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const PathParams& p, 
 
 // After a closest-hit query: one bounce of GetColor; a finished sample goes into the item's sums.
 __device__ __forceinline__ void bounce(Lane& L, Sample& S, const PathScene& s, const ShadeRecs& R, const float4* vnormals,
-                                       const Best& b)
+                                       const TestRec* tests, const Best& b)
 {
-    L.rays++;
     V3 col;
-    const int r = shade(s, R.prims, R.mats, R.xfs, vnormals, b, S, col);
+    const int r = shade(s, R.prims, R.mats, R.xfs, vnormals, tests, b, S, col);
     if (r != 0) {
         const bool hit = r == 1;
         L.ar += hit ? col.x : 0.0f;
@@ -794,12 +791,11 @@ __device__ __forceinline__ void bounce(Lane& L, Sample& S, const PathScene& s, c
 }
 
 template <bool STATS>
-__device__ __forceinline__ void flush_counts(const Lane& L, const Counters& cnt, const PathParams& p, int lane)
+__device__ __forceinline__ void flush_counts(unsigned long long wave_rays, const Counters& cnt, const PathParams& p,
+                                             int lane)
 {
     // one 64-bit add per wave for the ray count (and the optional traversal counters)
-    unsigned long long wr = L.rays;
-    for (int off = 32; off > 0; off >>= 1) wr += __shfl_down(wr, off);
-    if (lane == 0) atomicAdd(p.rays, wr);
+    if (lane == 0) atomicAdd(p.rays, wave_rays);
     if (STATS) {
         unsigned long long a = cnt.nodes, t = cnt.tris, q = cnt.sphs;
         for (int off = 32; off > 0; off >>= 1) {
@@ -826,7 +822,8 @@ __device__ __forceinline__ void flush_counts(const Lane& L, const Counters& cnt,
 // (the scene's records arrive through scalar loads) and shades it.
 template <bool CULL, bool LDS, bool STATS>
 __global__ void __launch_bounds__(256, RT_PATH_WAVES)
-    path_kernel(PathScene s, const CameraF* __restrict__ camp, PathParams p, const TestRec* __restrict__ tests,
+    path_kernel(PathScene s, const CameraF* __restrict__ camp, const PathParams* __restrict__ pp,
+                const TestRec* __restrict__ tests,
                 const RectRec* __restrict__ rects, const FrameRec* __restrict__ frames,
                 const PrimF* __restrict__ prims_g, const NodeF* __restrict__ nodes,
                 const Node4Q* __restrict__ nodes4, const GroupRec* __restrict__ groups, const XformF* __restrict__ xf,
@@ -835,7 +832,7 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
     extern __shared__ float4 lds_scene[];
     const ShadeRecs R = stage_scene<LDS>(s, prims_g, mats_g, xf, lds_scene);
     const int lane = threadIdx.x & 63;
-    const unsigned total = (unsigned)p.n_chunks * (unsigned)p.n_pad;
+    const unsigned total = (unsigned)pp->n_chunks * (unsigned)pp->n_pad;
     const int pln0 = s.n_bvh;
     Lane L;
     lane_init(L);
@@ -843,6 +840,7 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
     S.prev = -1;
     S.bounce = 0;
     Counters cnt{};
+    unsigned long long wave_rays = 0; // wave-uniform
     float exp_sink = 0.0f; // keeps the cost-experiment work alive (RT_EXP_*)
 
     while (true) {
@@ -854,23 +852,27 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
             // (they spilled, with the kernel's other arguments, into VGPR lanes and scratch)
             const CameraF* cp = camp;
             asm volatile("" : "+s"(cp));
-            refill(L, S, p, s, *cp, lane, total);
+            // the launch parameters likewise (a device copy, see run_path)
+            const PathParams* pq = pp;
+            asm volatile("" : "+s"(pq));
+            refill(L, S, *pq, s, *cp, lane, total);
         }
         if (!__any(L.active)) break;
         if (STATS) t1 = __builtin_readcyclecounter();
 #ifdef RT_EXP_DUP_START // cost experiment: a second camera sample on a copy
         if (L.live) {
             Sample S2 = S;
-            S2.rng.k0 ^= (unsigned)L.rays;
+            S2.rng.k0 ^= (unsigned)S.bounce;
             start_sample(*camp, L.fx, L.fy, S2);
             exp_sink += S2.o.x + S2.d.y;
         }
 #endif
+        wave_rays += (unsigned)__popcll(__ballot(L.live)); // one Scene.RayTrace per live lane
         if (L.live) {
-            Best b{__builtin_huge_valf(), -1, 0.0f, 0.0f};
+            Best b{__builtin_huge_valf(), -1};
 #ifdef RT_EXP_DUP_TRACE // cost experiment: a second closest-hit query from a perturbed origin
             {
-                Best b2{__builtin_huge_valf(), -1, 0.0f, 0.0f};
+                Best b2{__builtin_huge_valf(), -1};
                 unsigned u0 = 0, u1 = 0;
             trace_brute<CULL, false>(s, groups, tests, rects, frames, xf, S.o + v3(exp_sink * 1e-30f, 0, 0), S.d,
                                      S.prev, b2, u0, u1);
@@ -885,13 +887,13 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
 #ifdef RT_EXP_DUP_SHADE // cost experiment: a second bounce on a copy
             {
                 Sample S2 = S;
-                S2.rng.k0 ^= (unsigned)L.rays;
+                S2.rng.k0 ^= (unsigned)S.bounce;
                 V3 c2;
-                shade(s, R.prims, R.mats, R.xfs, vnormals, b, S2, c2);
+                shade(s, R.prims, R.mats, R.xfs, vnormals, tests, b, S2, c2);
                 exp_sink += c2.x + S2.d.x;
             }
 #endif
-            bounce(L, S, s, R, vnormals, b);
+            bounce(L, S, s, R, vnormals, tests, b);
         } else if (STATS) {
             t2 = __builtin_readcyclecounter();
         }
@@ -903,8 +905,8 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
             cnt.iters++;
         }
     }
-    if (exp_sink == 1234.5f) p.partial[0].x = exp_sink;
-    flush_counts<STATS>(L, cnt, p, lane);
+    if (exp_sink == 1234.5f) pp->partial[0].x = exp_sink;
+    flush_counts<STATS>(wave_rays, cnt, *pp, lane);
 }
 
 // BVH megakernel with decoupled traversal.  A loop iteration advances every traversing lane by
@@ -914,13 +916,15 @@ __global__ void __launch_bounds__(256, RT_PATH_WAVES)
 // divergent shading code is paid once per batch of finished queries.
 template <int WIDTH, int STACK, bool LDS, bool STATS>
 __global__ void __launch_bounds__(256, RT_BVH_WAVES)
-    path_kernel_bvh(PathScene s, const CameraF* __restrict__ camp, PathParams p, const TestRec* __restrict__ tests,
+    path_kernel_bvh(PathScene s, const CameraF* __restrict__ camp, const PathParams* __restrict__ pp,
+                    const TestRec* __restrict__ tests,
                     const RectRec* __restrict__ rects, const FrameRec* __restrict__ frames,
                     const PrimF* __restrict__ prims_g,
                     const NodeF* __restrict__ nodes, const Node4Q* __restrict__ nodes4,
                     const GroupRec* __restrict__ groups, const XformF* __restrict__ xf,
                     const MatF* __restrict__ mats_g, const float4* __restrict__ vnormals)
 {
+    const PathParams p = *pp;
     __shared__ int stack_mem[STACK * 256];
     extern __shared__ float4 lds_scene[];
     const TravStack stk{stack_mem + threadIdx.x, p.stack_ovf + blockIdx.x * 256 + threadIdx.x, (int)gridDim.x * 256};
@@ -935,20 +939,22 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
     S.prev = -1;
     S.bounce = 0;
     Counters cnt{};
+    unsigned long long wave_rays = 0; // wave-uniform
     // traversal state of the lane's current query
     bool trav = false, done = false;
     int ref = 0, sp = 0, k = 0, kend = 0; // [k, kend): primitives of the leaf being tested
     V3 id{0, 0, 0}, oi{0, 0, 0}; // 1/d and o/d of the query
-    Best b{__builtin_huge_valf(), -1, 0.0f, 0.0f};
+    Best b{__builtin_huge_valf(), -1};
 
     while (true) {
         const unsigned long long waiting = __ballot(!trav && (L.active || L.live));
         const unsigned long long busy = __ballot(trav);
         if (!waiting && !busy) break;
         if (!busy || __popcll(waiting) >= p.refill) {
+            wave_rays += (unsigned)__popcll(__ballot(done)); // one Scene.RayTrace per finished query
             if (done) { // the query finished: planes (outside the BVH), then one bounce
                 for (int i = pln0; i < pln0 + s.n_pln; i++) hit_plane(tests[i], i, S.o, S.d, S.prev, b);
-                bounce(L, S, s, R, vnormals, b);
+                bounce(L, S, s, R, vnormals, tests, b);
                 done = false;
             }
             refill(L, S, p, s, cam, lane, total);
@@ -962,7 +968,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                     k = (~ref) >> 3;
                     kend = k + ((~ref) & 7) + 1;
                 }
-                b = Best{__builtin_huge_valf(), -1, 0.0f, 0.0f};
+                b = Best{__builtin_huge_valf(), -1};
                 trav = true;
             }
         }
@@ -1032,7 +1038,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
             }
         }
     }
-    flush_counts<STATS>(L, cnt, p, lane);
+    flush_counts<STATS>(wave_rays, cnt, p, lane);
 }
 
 __global__ void accumulate_kernel(PathParams p, double* sum, uint32_t* samples, uint32_t* misses)
@@ -1111,7 +1117,7 @@ __global__ void colors_1spp_kernel(PathParams p, double* out)
     out[o + 2] = miss ? -1.0 : (double)v.z;
 }
 
-using PathKernel = void (*)(PathScene, const CameraF*, PathParams, const TestRec*, const RectRec*, const FrameRec*, const PrimF*,
+using PathKernel = void (*)(PathScene, const CameraF*, const PathParams*, const TestRec*, const RectRec*, const FrameRec*, const PrimF*,
                             const NodeF*, const Node4Q*, const GroupRec*, const XformF*, const MatF*, const float4*);
 
 template <bool CULL, bool LDS>
@@ -1186,8 +1192,8 @@ int path_blocks_per_cu(int variant, size_t dyn_lds, bool stats)
     return n;
 }
 
-hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams& p, int variant, int grid_blocks,
-                       hipStream_t stream, bool stats)
+hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams* d_params, int variant,
+                       int grid_blocks, hipStream_t stream, bool stats)
 {
     PathScene ps = make_path_scene(s);
     const int kernel = variant >> 1;
@@ -1197,7 +1203,7 @@ hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams
     ps.n_bvh = bvh ? s.pln0_bvh : grouped ? s.pln0_gr : s.pln0_bf;
     ps.n_slots = ps.n_bvh + s.n_pln;
     const CameraF* ca = d_cam;
-    PathParams pa = p;
+    const PathParams* pa = d_params;
     const TestRec* tests = bvh ? s.tests_bvh : grouped ? s.tests_gr : s.tests_bf;
     const RectRec* rects = grouped ? s.rects_gr : s.rects_bf;
     const FrameRec* frames = grouped ? s.frames_gr : s.frames_bf;

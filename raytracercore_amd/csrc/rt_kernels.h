@@ -43,8 +43,9 @@ constexpr int kStackOverflow = 40; // = RT_STACK_OVF (kernels_path.hip)
 int path_wide_stack();              // LDS entries of the wide BVH kernel's stack (RT_WIDE_STACK)
 size_t path_lds_bytes(const DevScene& s);   // dynamic LDS of the staged (lds) variants
 // Launch the persistent kernel; stats counts node visits / primitive tests (slower build).
-hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams& p, int variant, int grid_blocks,
-                       hipStream_t stream, bool stats);
+// The camera and the launch parameters are read from device memory (d_cam, d_params).
+hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams* d_params, int variant,
+                       int grid_blocks, hipStream_t stream, bool stats);
 int path_blocks_per_cu(int variant, size_t dyn_lds, bool stats);
 
 // partial -> fp64 planar accumulators (d_sum[3][w*h], d_samples, d_misses), added to.

@@ -145,6 +145,12 @@ struct rt_scene {
     CameraD camd{};
     CameraF camf{};
     DevBuf<CameraF> camf_d;     // the path kernels read the camera from device memory (not kernel arguments)
+    // ... and their launch parameters, from a ring of device slots filled from pinned host slots
+    // (a slot is reused kParamRing launches later, long after its launch has read it)
+    static constexpr int kParamRing = 256;
+    DevBuf<PathParams> params_d;
+    PathParams* params_h = nullptr;
+    unsigned params_next = 0;
     bool has_camera = false;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -152,6 +158,7 @@ struct rt_scene {
 
     ~rt_scene()
     {
+        if (params_h) (void)hipHostFree(params_h);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         if (stream) (void)hipStreamDestroy(stream);
@@ -1045,7 +1052,14 @@ int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t
         p.stack_ovf = s->stack_ovf.p;
     }
     HIP_TRY(hipEventRecord(s->ev0, stream));
-    HIP_TRY(launch_path(s->dev, s->camf_d.p, p, s->variant, grid, stream, s->stats_on));
+    if (!s->params_h) {
+        HIP_TRY(hipHostMalloc(&s->params_h, sizeof(PathParams) * rt_scene::kParamRing, hipHostMallocDefault));
+        HIP_TRY(s->params_d.reserve(rt_scene::kParamRing));
+    }
+    const unsigned slot = s->params_next++ % rt_scene::kParamRing;
+    s->params_h[slot] = p;
+    HIP_TRY(hipMemcpyAsync(s->params_d.p + slot, s->params_h + slot, sizeof(PathParams), hipMemcpyHostToDevice, stream));
+    HIP_TRY(launch_path(s->dev, s->camf_d.p, s->params_d.p + slot, s->variant, grid, stream, s->stats_on));
     HIP_TRY(hipEventRecord(s->ev1, stream));
     return RT_OK;
 }
