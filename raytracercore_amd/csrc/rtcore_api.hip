@@ -705,7 +705,8 @@ int upload_scene(rt_scene* s)
     int nr[3] = {flat.nr[0], flat.nr[1], flat.nr[2]}, nt = flat.nt, ns = flat.ns, np = 0;
     for (int i = 0; i < n; i++) np += kind_of[i] == 5;
     // groups: subtrees of the SAH BVH with at most kGroupMax primitives (small scenes only)
-    constexpr int kGroupMax = 8;
+    int kGroupMax = 4; // die.txt 1080p grouped: 2 -> 50.1 ms, 3 -> 47.6, 4 -> 46.4, 6 -> 48.4, 8 -> 48.4, 16 -> 50.7
+    if (const char* e = getenv("RTCORE_GROUP_MAX")) kGroupMax = std::max(1, atoi(e)); // tuning
     std::vector<std::vector<int>> cut;
     if ((int)all.size() <= 4096 && !s->sah.order.empty()) {
         std::function<void(int, std::vector<int>&)> leaves = [&](int ref, std::vector<int>& out) {
