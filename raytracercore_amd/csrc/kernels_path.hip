@@ -655,7 +655,7 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
 #define RT_PATH_WAVES 6 // minimum waves per SIMD the register allocator must allow (brute force)
 #endif
 #ifndef RT_WIDE_STACK
-#define RT_WIDE_STACK 40 // LDS entries of the wide BVH kernel's traversal stack (then global overflow)
+#define RT_WIDE_STACK 32 // LDS entries of the wide BVH kernel's traversal stack (then global overflow)
 #endif
 #ifndef RT_LEAF_STEP
 #define RT_LEAF_STEP 2 // leaf primitives tested per BVH traversal step
@@ -687,6 +687,12 @@ __device__ __forceinline__ ShadeRecs stage_scene(const PathScene& s, const PrimF
     __syncthreads();
     return ShadeRecs{reinterpret_cast<const PrimF*>(lds_scene), reinterpret_cast<const MatF*>(lds_scene + n_p),
                      reinterpret_cast<const XformF*>(lds_scene + n_p + n_m)};
+}
+
+__device__ __forceinline__ int scene_lds_float4s(const PathScene& s)
+{
+    return s.n_slots * (int)(sizeof(PrimF) / 16) + s.n_ids * (int)(sizeof(MatF) / 16) +
+           s.n_xf * (int)(sizeof(XformF) / 16);
 }
 
 // One lane's work: the open work item (a chunk of samples of one pixel), its running sums and
@@ -930,6 +936,14 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
     const TravStack stk{stack_mem + threadIdx.x, p.stack_ovf + blockIdx.x * 256 + threadIdx.x, (int)gridDim.x * 256};
     const CameraF cam = *camp;
     const ShadeRecs R = stage_scene<LDS>(s, prims_g, mats_g, xf, lds_scene);
+    // hot wide nodes after the staged shading records (dynamic LDS; see path_lds_bytes)
+    Node4Q* lds_hot = reinterpret_cast<Node4Q*>(lds_scene + (LDS ? scene_lds_float4s(s) : 0));
+    if (WIDTH == 4 && s.n_hot4 > 0) {
+        const float4* src = reinterpret_cast<const float4*>(s.hot4);
+        float4* dst = reinterpret_cast<float4*>(lds_hot);
+        for (int i = threadIdx.x; i < s.n_hot4 * 4; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+    }
     const int lane = threadIdx.x & 63;
     const unsigned total = (unsigned)p.n_chunks * (unsigned)p.n_pad;
     const int pln0 = s.n_bvh;
@@ -996,7 +1010,9 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                 k += RT_LEAF_STEP;
                 pop = k >= kend;
             } else if (WIDTH == 4) {
-                wide_visit<STACK>(nodes4[ref], id, oi, b.t, ref, sp, stk, pop);
+                // the top of the tree comes from LDS, the rest from global memory
+                const Node4Q q = (ref & RT_HOT_BIT) ? lds_hot[ref & ~RT_HOT_BIT] : nodes4[ref];
+                wide_visit<STACK>(q, id, oi, b.t, ref, sp, stk, pop);
                 if (STATS) cnt.nodes++;
             } else {
                 const NodeF n = nodes[ref];
@@ -1182,11 +1198,24 @@ size_t path_lds_bytes(const DevScene& s)
 
 int path_variant(int kernel, bool lds) { return kernel * 2 + (lds ? 1 : 0); }
 
+bool hot_nodes_enabled()
+{
+    static const bool on = !(getenv("RTCORE_HOT_NODES") && getenv("RTCORE_HOT_NODES")[0] == '0'); // A/B switch
+    return on;
+}
+
+size_t path_dyn_lds(const DevScene& s, int variant)
+{
+    size_t b = (variant & 1) ? path_lds_bytes(s) : 0;
+    if ((variant >> 1) == 3 && s.n_hot4 > 0 && hot_nodes_enabled()) b += (size_t)s.n_hot4 * sizeof(Node4Q);
+    return b;
+}
+
 int path_blocks_per_cu(int variant, size_t dyn_lds, bool stats)
 {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(pick(variant, stats)), 256,
-                                                     (variant & 1) ? dyn_lds : 0) != hipSuccess ||
+                                                     dyn_lds) != hipSuccess ||
         n < 1)
         n = 1;
     return n;
@@ -1197,7 +1226,16 @@ hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams
 {
     PathScene ps = make_path_scene(s);
     const int kernel = variant >> 1;
-    if (kernel == 3) ps.root = s.root4; // the wide kernel walks the collapsed tree
+    ps.hot4 = nullptr;
+    ps.n_hot4 = 0;
+    if (kernel == 3) { // the wide kernel walks the collapsed tree, its top from the hot table
+        ps.root = s.root4;
+        if (s.n_hot4 > 0 && hot_nodes_enabled()) {
+            ps.root = s.root4_hot;
+            ps.hot4 = s.hot4;
+            ps.n_hot4 = s.n_hot4;
+        }
+    }
     const bool grouped = kernel == 1, bvh = kernel >= 2;
     ps.n_groups = grouped ? s.n_groups_gr : 1;
     ps.n_bvh = bvh ? s.pln0_bvh : grouped ? s.pln0_gr : s.pln0_bf;
@@ -1215,7 +1253,7 @@ hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams
     const MatF* mats = s.mats;
     const float4* vn = s.vnormals;
     void* args[] = {&ps, &ca, &pa, &tests, &rects, &frames, &prims, &nodes, &nodes4, &groups, &xf, &mats, &vn};
-    const size_t dyn = (variant & 1) ? path_lds_bytes(s) : 0;
+    const size_t dyn = path_dyn_lds(s, variant);
     return hipLaunchKernel(reinterpret_cast<const void*>(pick(variant, stats)), dim3(grid_blocks), dim3(256), args, dyn,
                            stream);
 }

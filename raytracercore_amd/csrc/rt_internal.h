@@ -148,6 +148,8 @@ struct alignas(16) TestRec {
     float4 r0, r1, r2, meta;
 };
 
+struct Node4Q;
+
 // Scalar fields of the path kernel (pointers are passed as separate __restrict__ arguments
 // so that the wave-uniform primitive loop is served by scalar loads).
 struct PathScene {
@@ -160,6 +162,8 @@ struct PathScene {
     int32_t n_xf;                // XformF records
     int32_t n_groups;            // brute force: GroupRec records
     int32_t root;                // child reference of the BVH root
+    const Node4Q* hot4;          // wide kernel: the top nodes, staged in LDS (child refs | RT_HOT_BIT)
+    int32_t n_hot4;
     int32_t width;               // frame width (RNG pixel index)
     int32_t recursion;
     int32_t debug_geom;
@@ -183,6 +187,9 @@ struct alignas(16) NodeF {      // 64 B: both children's boxes
 // Child references as in NodeF (>= 0 wide-node index, < 0 leaf code); unused slots are
 // RT_NODE4_EMPTY with an inverted box.
 #define RT_NODE4_EMPTY ((int32_t)0x80000000)
+// A child reference with this bit set names a node of the hot table (the top of the wide tree in
+// breadth-first order, copied into LDS by the wide kernel) instead of the global node array.
+#define RT_HOT_BIT 0x40000000
 struct alignas(16) Node4Q {
     float4 a, b, c, d;
 };
@@ -286,6 +293,9 @@ struct DevScene {
     const Node4Q* nodes4;       // the same tree collapsed to 4-wide quantised nodes
     int32_t n_nodes4;
     int32_t root4;
+    const Node4Q* hot4;         // the top n_hot4 wide nodes, breadth-first, refs among them | RT_HOT_BIT
+    int32_t n_hot4;
+    int32_t root4_hot;          // root reference when the hot table is used
     const XformF* xf;
     const MatF* mats;
     const float4* vnormals;     // 3 per primitive ID (HasNormals triangles)

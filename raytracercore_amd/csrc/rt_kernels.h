@@ -42,6 +42,7 @@ int path_variant(int kernel, bool lds);
 constexpr int kStackOverflow = 40; // = RT_STACK_OVF (kernels_path.hip)
 int path_wide_stack();              // LDS entries of the wide BVH kernel's stack (RT_WIDE_STACK)
 size_t path_lds_bytes(const DevScene& s);   // dynamic LDS of the staged (lds) variants
+size_t path_dyn_lds(const DevScene& s, int variant); // all dynamic LDS of a variant (+ the wide kernel's hot nodes)
 // Launch the persistent kernel; stats counts node visits / primitive tests (slower build).
 // The camera and the launch parameters are read from device memory (d_cam, d_params).
 hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams* d_params, int variant,

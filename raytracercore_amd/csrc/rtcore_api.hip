@@ -15,6 +15,7 @@
 #include <functional>
 #include <memory>
 #include <string>
+#include <unordered_map>
 #include <thread>
 #include <vector>
 
@@ -125,6 +126,7 @@ struct rt_scene {
     double grouped_measured = 0; // calibrated brute-force cost ratio flat / grouped (AUTO picks grouped above 1.25)
     DevBuf<NodeF> nodes;
     DevBuf<Node4Q> nodes4;
+    DevBuf<Node4Q> hot4;        // top of the wide tree, breadth-first, staged in LDS by the wide kernel
     DevBuf<XformF> xf;
     DevBuf<MatF> mats;
     DevBuf<float4> vnormals;
@@ -823,7 +825,54 @@ int upload_scene(rt_scene* s)
                       (size_t)s->bvh.n_nodes2 * sizeof(NodeF) + (size_t)s->bvh.n_nodes4 * sizeof(Node4Q) +
                       xf.size() * sizeof(XformF) + mats.size() * sizeof(MatF) + vn.size() * sizeof(float4);
 
+    // Hot table: the first kHot wide nodes in breadth-first order from the root, their references
+    // to each other rewritten to RT_HOT_BIT | hot index (the global tree is unchanged).
+    std::vector<Node4Q> hot;
+    int root4_hot = s->bvh.root4;
+    {
+        int k_hot = 128; // with the 32-entry LDS stack: 4 blocks x (32 + 8) KB per CU
+        if (const char* e = getenv("RTCORE_HOT_NODES")) k_hot = std::max(0, std::min(1024, atoi(e)));
+        if (k_hot > 0 && s->bvh.root4 >= 0 && s->bvh.n_nodes4 > 0) {
+            std::vector<Node4Q> all4((size_t)s->bvh.n_nodes4);
+            HIP_TRY(hipMemcpy(all4.data(), s->nodes4.p, all4.size() * sizeof(Node4Q), hipMemcpyDeviceToHost));
+            std::vector<int> order{s->bvh.root4};
+            std::unordered_map<int, int> slot_of{{s->bvh.root4, 0}};
+            for (size_t q = 0; q < order.size() && (int)order.size() < k_hot; q++) {
+                const Node4Q& nd = all4[order[q]];
+                int32_t ch[4];
+                std::memcpy(&ch[0], &nd.c.z, 4);
+                std::memcpy(&ch[1], &nd.c.w, 4);
+                std::memcpy(&ch[2], &nd.d.x, 4);
+                std::memcpy(&ch[3], &nd.d.y, 4);
+                for (int c : ch)
+                    if (c >= 0 && (int)order.size() < k_hot && !slot_of.count(c)) {
+                        slot_of[c] = (int)order.size();
+                        order.push_back(c);
+                    }
+            }
+            for (int g : order) {
+                Node4Q nd = all4[g];
+                float* refs[4] = {&nd.c.z, &nd.c.w, &nd.d.x, &nd.d.y};
+                for (float* r : refs) {
+                    int32_t c;
+                    std::memcpy(&c, r, 4);
+                    auto it = c >= 0 ? slot_of.find(c) : slot_of.end();
+                    if (it != slot_of.end()) {
+                        c = RT_HOT_BIT | it->second;
+                        std::memcpy(r, &c, 4);
+                    }
+                }
+                hot.push_back(nd);
+            }
+            root4_hot = RT_HOT_BIT | 0;
+        }
+    }
+    HIP_TRY(s->hot4.upload(hot));
+
     DevScene& d = s->dev;
+    d.hot4 = s->hot4.p;
+    d.n_hot4 = (int)hot.size();
+    d.root4_hot = root4_hot;
     d.tests_bf = s->tests_bf.p;
     d.tests_bvh = s->tests_bvh.p;
     d.rects_bf = s->rects_bf.p;
@@ -917,13 +966,13 @@ int resolve_traversal(rt_scene* s)
     // the choice for A/B measurements).
     const size_t lds = path_lds_bytes(s->dev);
     const int plain = path_variant(kernel, false), staged = path_variant(kernel, true);
-    const int occ_plain = path_blocks_per_cu(plain, 0, false);
-    const int occ_staged = lds <= 64 * 1024 ? path_blocks_per_cu(staged, lds, false) : 0;
+    const int occ_plain = path_blocks_per_cu(plain, path_dyn_lds(s->dev, plain), false);
+    const int occ_staged = lds <= 64 * 1024 ? path_blocks_per_cu(staged, path_dyn_lds(s->dev, staged), false) : 0;
     bool use_lds = occ_staged >= occ_plain;
     if (const char* e = getenv("RTCORE_PATH_LDS")) use_lds = e[0] == '1' && occ_staged > 0;
     s->variant = use_lds ? staged : plain;
     s->blocks_per_cu = use_lds ? occ_staged : occ_plain;
-    if (s->stats_on) s->stats_blocks_per_cu = path_blocks_per_cu(s->variant, lds, true);
+    if (s->stats_on) s->stats_blocks_per_cu = path_blocks_per_cu(s->variant, path_dyn_lds(s->dev, s->variant), true);
     return RT_OK;
 }
 
@@ -1490,7 +1539,7 @@ int rt_scene_set_stats(rt_scene* s, int32_t enable)
     if (enable) {
         HIP_TRY(s->stats_buf.reserve(RT_STATS_COUNT));
         HIP_TRY(hipMemset(s->stats_buf.p, 0, RT_STATS_COUNT * sizeof(unsigned long long)));
-        s->stats_blocks_per_cu = path_blocks_per_cu(s->variant, path_lds_bytes(s->dev), true);
+        s->stats_blocks_per_cu = path_blocks_per_cu(s->variant, path_dyn_lds(s->dev, s->variant), true);
     }
     s->stats_on = enable != 0;
     return RT_OK;
