@@ -759,8 +759,12 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const PathParams& p, 
                     L.fx = p.x0 + px;
                     L.fy = p.band > 0 ? p.y0 + ((py / p.band) * p.band_stride + p.band_offset) * p.band + py % p.band
                                       : p.y0 + py;
+#ifdef RT_EXP_CHEAP_PKEY // cost experiment: no pixel-key hashing
+                    L.pkey = rt_key2{(unsigned)L.fx * 0x9E3779B9u, (unsigned)L.fy};
+#else
                     L.pkey = rt_rng_pixel_key(p.seed_key, (unsigned long long)L.fy * (unsigned long long)s.width +
                                                               (unsigned long long)L.fx);
+#endif
                 }
             }
         }
@@ -772,8 +776,20 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const PathParams& p, 
         }
     }
     if (L.active && L.item_open && !L.live && L.s_next < L.s_end) {
+#ifdef RT_EXP_CHEAP_SKEY // cost experiment: no sample-key hashing
+        S.rng = rt_rng{L.pkey.a + (unsigned)L.s_next * 0x85EBCA6Bu, L.pkey.b};
+#else
         S.rng = rt_rng_from_pixel_key(L.pkey, p.sample_base + (unsigned long long)L.s_next);
+#endif
+#ifdef RT_EXP_CHEAP_CAMERA // cost experiment: a fixed camera ray per pixel (no draws, no normalise)
+        S.o = xyz(cam.position);
+        S.d = v3(cam.look.x + (float)L.fx * 1e-4f, cam.look.y + (float)L.fy * 1e-4f, cam.look.z);
+        S.tint = v3(1.0f, 1.0f, 1.0f);
+        S.bounce = 0;
+        S.prev = -1;
+#else
         start_sample(cam, L.fx, L.fy, S);
+#endif
         L.live = true;
     }
 }
