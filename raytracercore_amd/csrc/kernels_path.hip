@@ -652,7 +652,7 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
 }
 
 #ifndef RT_PATH_WAVES
-#define RT_PATH_WAVES 6 // minimum waves per SIMD the register allocator must allow (brute force)
+#define RT_PATH_WAVES 7 // minimum waves per SIMD the register allocator must allow (brute force; 6 -> 7: C2 28.4 -> 27.5 ms)
 #endif
 #ifndef RT_WIDE_STACK
 #define RT_WIDE_STACK 32 // LDS entries of the wide BVH kernel's traversal stack (then global overflow)
@@ -700,10 +700,10 @@ __device__ __forceinline__ int scene_lds_float4s(const PathScene& s)
 struct Lane {
     bool active, item_open, live;
     unsigned item;
-    int fx, fy, s_next, s_end;
+    int fx, fy, s_next;
     rt_key2 pkey; // rt_rng_pixel_key of the open item's pixel
     float ar, ag, ab;
-    unsigned n_s, n_m;
+    unsigned cnt; // item bookkeeping: samples (bits 0-7) | misses (8-15) | samples left (16-31)
     unsigned pool_next, pool_end;
 };
 
@@ -712,10 +712,10 @@ __device__ __forceinline__ void lane_init(Lane& L)
     L.active = true;
     L.item_open = L.live = false;
     L.item = 0;
-    L.fx = L.fy = L.s_next = L.s_end = 0;
+    L.fx = L.fy = L.s_next = 0;
     L.pkey = rt_key2{0u, 0u};
     L.ar = L.ag = L.ab = 0.0f;
-    L.n_s = L.n_m = 0;
+    L.cnt = 0;
     L.pool_next = L.pool_end = 0;
 }
 
@@ -725,9 +725,9 @@ __device__ __forceinline__ void lane_init(Lane& L)
 __device__ __forceinline__ void refill(Lane& L, Sample& S, const PathParams& p, const PathScene& s, const CameraF& cam, int lane,
                                       unsigned total)
 {
-    const bool need = L.active && !L.live && (!L.item_open || L.s_next >= L.s_end);
+    const bool need = L.active && !L.live && (!L.item_open || L.cnt < 65536u);
     if (need && L.item_open) {
-        p.partial[L.item] = make_float4(L.ar, L.ag, L.ab, __uint_as_float(L.n_s | (L.n_m << 16)));
+        p.partial[L.item] = make_float4(L.ar, L.ag, L.ab, __uint_as_float((L.cnt & 0xFFu) | ((L.cnt & 0xFF00u) << 8)));
         L.item_open = false;
     }
     const unsigned long long m = __ballot(need);
@@ -753,9 +753,8 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const PathParams& p, 
                 if (px < p.w && py < p.h && c * p.chunk < p.spp) {
                     L.item_open = true;
                     L.s_next = c * p.chunk;
-                    L.s_end = min(p.spp, L.s_next + p.chunk);
+                    L.cnt = (unsigned)(min(p.spp, L.s_next + p.chunk) - L.s_next) << 16; // chunk <= 64
                     L.ar = L.ag = L.ab = 0.0f;
-                    L.n_s = L.n_m = 0;
                     L.fx = p.x0 + px;
                     L.fy = p.band > 0 ? p.y0 + ((py / p.band) * p.band_stride + p.band_offset) * p.band + py % p.band
                                       : p.y0 + py;
@@ -775,7 +774,7 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const PathParams& p, 
             L.pool_next += k;
         }
     }
-    if (L.active && L.item_open && !L.live && L.s_next < L.s_end) {
+    if (L.active && L.item_open && !L.live && L.cnt >= 65536u) {
 #ifdef RT_EXP_CHEAP_SKEY // cost experiment: no sample-key hashing
         S.rng = rt_rng{L.pkey.a + (unsigned)L.s_next * 0x85EBCA6Bu, L.pkey.b};
 #else
@@ -805,8 +804,7 @@ __device__ __forceinline__ void bounce(Lane& L, Sample& S, const PathScene& s, c
         L.ar += hit ? col.x : 0.0f;
         L.ag += hit ? col.y : 0.0f;
         L.ab += hit ? col.z : 0.0f;
-        L.n_s += hit ? 1u : 0u; // arithmetic, not a selected counter (that would live in scratch)
-        L.n_m += hit ? 0u : 1u;
+        L.cnt += hit ? 1u - 65536u : 256u - 65536u; // one more sample or miss, one fewer left
         L.s_next++;
         L.live = false;
     }
