@@ -157,8 +157,10 @@ typedef enum rt_bvh_builder {
 
 /* rt_scene_get_build_stats: [0] host preparation ms, [1] BVH build ms (wall, either
    builder), [2] upload ms, [3] GPU builder device ms, [4] PLOC rounds, [5] wide nodes,
-   [6] wide-tree stack need */
-#define RT_BUILD_STATS_COUNT 7
+   [6] wide-tree stack need; flat brute-force layout: [7] single world rectangles,
+   [8] world boxes, [9] frames, [10] frame boxes, [11] rectangles tested one by one in
+   frames, [12] other triangles, [13] spheres, [14] hot wide nodes staged in LDS */
+#define RT_BUILD_STATS_COUNT 15
 
 /* ---------------------------------------------------------------- library ---- */
 int rt_abi_version(void);

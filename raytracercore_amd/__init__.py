@@ -28,7 +28,9 @@ RT_FLAG_MIRROR, RT_FLAG_TWOSIDED, RT_FLAG_INVERT, RT_FLAG_HASNORMALS, RT_FLAG_TR
 RT_CAMERA_FRUSTUM, RT_CAMERA_ORTHO = 0, 1
 RT_TRAVERSAL_AUTO, RT_TRAVERSAL_BRUTE, RT_TRAVERSAL_BVH, RT_TRAVERSAL_BVH2, RT_TRAVERSAL_GROUPED = 0, 1, 2, 3, 4
 RT_BVH_BUILDER_AUTO, RT_BVH_BUILDER_HOST, RT_BVH_BUILDER_GPU = 0, 1, 2
-BUILD_STAT_NAMES = ("prepare_ms", "bvh_ms", "upload_ms", "gpu_build_ms", "ploc_rounds", "wide_nodes", "stack_need")
+BUILD_STAT_NAMES = ("prepare_ms", "bvh_ms", "upload_ms", "gpu_build_ms", "ploc_rounds", "wide_nodes", "stack_need",
+                    "flat_rects", "flat_boxes", "flat_frames", "flat_frame_boxes", "flat_frame_rects", "flat_tris",
+                    "flat_spheres", "hot_nodes")
 
 
 class RtError(RuntimeError):

@@ -337,7 +337,8 @@ def test_ragged_tiles_and_spp(rc, scenes, w, h, spp):
 
 # Closed boxes under every culling rule the box test folds into its keep masks: one-sided seen
 # from outside (entry faces), inverted one-sided in a rotated frame (exit faces only), two-sided
-# in a skewed frame (both), and an inverted room around everything (exit faces, as bounce.txt).
+# in a skewed frame (both), an open emissive box (five faces: a placeholder slot), a plane after
+# the box slots (per-order plane offsets), and an inverted room around everything (exit faces).
 BOX_SCENE = """size 48 36
 camera 0 -6 1.5, 0 0 0, 0 0 1, 70
 ambient color .3 .3 .3
@@ -362,6 +363,12 @@ emission 1 .8 .6
 cube 0 0 0 1 1 1 all
 emission 0 0 0
 poptransform
+emission .6 .6 .6
+twosided true
+cube 0 1.5 -.5 1 .5 .5 not -z
+emission 0 0 0
+diffuse .3 .3 .3
+plane 3 0 1 0
 invert true
 twosided false
 cube 0 0 0 12 12 12 all
@@ -399,3 +406,20 @@ def test_closed_boxes_match_oracle(rc):
     err = np.sum((mean_g - mean_o) ** 2, axis=-1)[both]
     assert float(err.mean()) < 1e-4, f"mean squared L2 error {err.mean():.3g}"
     assert abs(rays - rays_o) <= 0.01 * rays_o
+
+
+@pytest.mark.parametrize("name,expect", [
+    # the cut-out corner's two faces stay rectangles; the inverted room and the open light box are
+    # world boxes; the rotated cube is one frame with its box; three spheres (one transformed)
+    ("bounce.txt", dict(flat_rects=2, flat_boxes=2, flat_frames=1, flat_frame_boxes=1, flat_frame_rects=0,
+                        flat_tris=0, flat_spheres=3)),
+    # the die is one world box; 2 light spheres and 21 pips
+    ("die.txt", dict(flat_rects=0, flat_boxes=1, flat_frames=0, flat_tris=0, flat_spheres=23)),
+    ("BOX", dict(flat_rects=0, flat_boxes=3, flat_frames=2, flat_frame_boxes=2, flat_frame_rects=0, flat_tris=0,
+                 flat_spheres=0)),
+])
+def test_brute_layout(rc, scenes, name, expect):
+    """The flat brute-force order's decomposition into rectangles, boxes and frames."""
+    scene = rc.SceneLoader.from_text(BOX_SCENE) if name == "BOX" else scenes[name]
+    st = rc.GpuRaytracer(scene, 0, size=(32, 24), traversal=rc.RT_TRAVERSAL_BRUTE).build_stats()
+    assert {k: int(st[k]) for k in expect} == expect
