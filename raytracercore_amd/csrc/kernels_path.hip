@@ -654,6 +654,9 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
 #ifndef RT_PATH_WAVES
 #define RT_PATH_WAVES 7 // minimum waves per SIMD the register allocator must allow (brute force; 6 -> 7: C2 28.4 -> 27.5 ms)
 #endif
+#ifndef RT_GROUPED_WAVES
+#define RT_GROUPED_WAVES 7 // the same for the grouped brute-force kernel
+#endif
 #ifndef RT_WIDE_STACK
 #define RT_WIDE_STACK 32 // LDS entries of the wide BVH kernel's traversal stack (then global overflow)
 #endif
@@ -841,7 +844,7 @@ __device__ __forceinline__ void flush_counts(unsigned long long wave_rays, const
 // Brute-force megakernel: every loop iteration issues one closest-hit query per live lane
 // (the scene's records arrive through scalar loads) and shades it.
 template <bool CULL, bool LDS, bool STATS>
-__global__ void __launch_bounds__(256, RT_PATH_WAVES)
+__global__ void __launch_bounds__(256, CULL ? RT_GROUPED_WAVES : RT_PATH_WAVES)
     path_kernel(PathScene s, const CameraF* __restrict__ camp, const PathParams* __restrict__ pp,
                 const TestRec* __restrict__ tests,
                 const RectRec* __restrict__ rects, const FrameRec* __restrict__ frames,
