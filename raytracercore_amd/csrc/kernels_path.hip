@@ -594,17 +594,17 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
     const float cs = -dot(rough, S.d);
     float cos_out = 0.0f, ior_ratio = 0.0f;
     if (((refr_lum > 0.0f) | (spec_lum > 0.0f)) && M.ior != 0.0f && cs >= 0.0f) { // Raytracer.cs:120-161
-        const float ior_in = inside ? M.ior : s.air_ior;
-        const float ior_out = inside ? s.air_ior : M.ior;
-        ior_ratio = ior_in * rcp(ior_out);
+        ior_ratio = inside ? M.eta_exit : M.eta_enter; // eta = iorIn / iorOut
         const float sin_out = ior_ratio * fsqrt(1.0f - cs * cs);
         if (sin_out >= 1.0f) {
             refr_lum = 0.0f;
         } else {
             cos_out = fsqrt(1.0f - sin_out * sin_out);
-            const float rs = (ior_out * cs - ior_in * cos_out) * rcp(ior_out * cs + ior_in * cos_out);
-            const float rp = (ior_in * cs - ior_out * cos_out) * rcp(ior_in * cs + ior_out * cos_out);
-            const float ratio = (rs * rs + rp * rp) * 0.5f;
+            // unpolarised Fresnel with numerator and denominator divided by iorOut:
+            // rs = (cs - eta co) / (cs + eta co), rp = (eta cs - co) / (eta cs + co), one reciprocal
+            const float ra = fmaf(-ior_ratio, cos_out, cs), rb = fmaf(ior_ratio, cos_out, cs);
+            const float pa = fmaf(ior_ratio, cs, -cos_out), pb = fmaf(ior_ratio, cs, cos_out);
+            const float ratio = (ra * ra * pb * pb + pa * pa * rb * rb) * rcp(rb * rb * pb * pb) * 0.5f;
             spec_lum *= ratio;
             refr_lum *= 1.0f - ratio;
         }

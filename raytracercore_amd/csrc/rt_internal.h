@@ -119,6 +119,8 @@ struct alignas(16) MatF {       // per primitive ID, 80 B
     float ior;                  // RefractiveIndex
     uint32_t flags;
     float inv_shininess;        // 1 / Shininess (RandomShine's exponent)
+    float eta_enter, eta_exit;  // AirRefractiveIndex / RefractiveIndex and its inverse (0 when no IOR)
+    float pad[2];
 };
 
 // A group of the brute-force slot order (64 B): its primitives' box (fp32, rounded outward) and

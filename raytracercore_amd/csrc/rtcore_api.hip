@@ -814,6 +814,10 @@ int upload_scene(rt_scene* s)
         m.ior = (float)p.ior;
         m.flags = p.flags;
         m.inv_shininess = (float)(1.0 / p.shininess);
+        // Raytracer.cs:127-133: ratio = iorIn / iorOut, air outside, swapped when the hit is Inside
+        m.eta_enter = p.ior != 0 ? (float)(s->params.air_ior / p.ior) : 0.0f;
+        m.eta_exit = p.ior != 0 ? (float)(p.ior / s->params.air_ior) : 0.0f;
+        m.pad[0] = m.pad[1] = 0.0f;
     }
     HIP_TRY(s->prims_d.upload(pd));
     HIP_TRY(s->xf_d.upload(xd));
