@@ -658,13 +658,13 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
 #define RT_GROUPED_WAVES 7 // the same for the grouped brute-force kernel
 #endif
 #ifndef RT_WIDE_STACK
-#define RT_WIDE_STACK 32 // LDS entries of the wide BVH kernel's traversal stack (then global overflow)
+#define RT_WIDE_STACK 24 // LDS entries of the wide BVH kernel's traversal stack (then global overflow)
 #endif
 #ifndef RT_LEAF_STEP
 #define RT_LEAF_STEP 2 // leaf primitives tested per BVH traversal step
 #endif
 #ifndef RT_BVH_WAVES
-#define RT_BVH_WAVES 4 // the same for the BVH kernel (the wide kernel's 40 KB LDS stack caps it at 4)
+#define RT_BVH_WAVES 5 // the same for the BVH kernels (C4: 4 waves with a 40-entry LDS stack 80.7 ms, 5 waves with 24 entries 72.0 ms)
 #endif
 
 // LDS staging of the shading records (PrimF per slot, MatF per ID, XformF): the per-lane gathers
