@@ -425,14 +425,16 @@ def test_brute_layout(rc, scenes, name, expect):
     assert {k: int(st[k]) for k in expect} == expect
 
 
-def test_full_frame_1080p_against_oracle(rc, scenes):
+@pytest.mark.parametrize("name", ["bounce.txt", "die.txt"])
+def test_full_frame_1080p_against_oracle(rc, scenes, name):
     """The BASELINE tolerance on the bench workload itself (configs[1]): bounce.txt at 1920x1080,
-    camera 0, 256 samples per pixel, fp32 kernel against the fp64 oracle under the shared RNG (the
-    oracle renders with the reference's tile scheduler on the host cores, ~25 s on 16 threads).  Mean over pixels of the squared L2 RGB
+    camera 0, 256 samples per pixel (and die.txt, with depth of field, at the same size), fp32
+    kernel against the fp64 oracle under the shared RNG (the oracle renders with the reference's
+    tile scheduler on the host cores, ~25 s and ~7 s on 16 threads).  Mean over pixels of the squared L2 RGB
     error of the per-pixel mean < 1e-4; the largest single-pixel error is reported."""
     import os
 
-    scene = scenes["bounce.txt"]
+    scene = scenes[name]
     W, H, spp = 1920, 1080, 256
     gpu = rc.GpuRaytracer(scene, 0, size=(W, H))
     s, n, m, rays = gpu.render_tile(0, 0, W, H, spp, seed=0)
@@ -444,7 +446,7 @@ def test_full_frame_1080p_against_oracle(rc, scenes):
     mean_g = s / np.maximum(n, 1)[..., None]
     mean_o = so / np.maximum(no, 1)[..., None]
     err = np.sum((mean_g - mean_o) ** 2, axis=-1)[both]
-    print(f"1080p x {spp} spp: mean squared L2 error {err.mean():.3g}, max {err.max():.3g}, "
+    print(f"{name} 1080p x {spp} spp: mean squared L2 error {err.mean():.3g}, max {err.max():.3g}, "
           f"rays gpu {rays} oracle {rays_o} ({secs:.1f} s on {used} threads)")
     assert float(err.mean()) < 1e-4
     assert abs(rays - rays_o) <= 0.01 * rays_o
