@@ -183,6 +183,13 @@ int rt_scene_get_build_stats(const rt_scene* scene, double* out, int32_t n);
    child box contains the primitives below it, each primitive in exactly one leaf, depth and
    stack within what the kernels were sized for).  RT_ERR_STATE with the finding otherwise. */
 int rt_scene_check_bvh(rt_scene* scene);
+/* Host only (no device needed): the decomposition the brute-force kernels would test for these
+   primitives -- out[0..9] = flat order: single world rectangles, world boxes (five or six faces of
+   an axis-aligned box), frames (parallelograms along one affine frame's axes), frame boxes,
+   rectangles tested one by one in frames, other triangles, spheres, planes; then the grouped
+   order's group count and its slot count.  Copies min(n_out, 10) values. */
+#define RT_LAYOUT_COUNT 10
+int rt_debug_brute_layout(const rt_prim* prims, int32_t n_prims, int32_t* out, int32_t n_out);
 
 /* ------------------------------------------------------- host-buffer renders --- */
 /*

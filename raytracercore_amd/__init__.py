@@ -183,6 +183,21 @@ class SceneLoader:
             return SceneLoader.from_text(f.read())
 
 
+LAYOUT_NAMES = ("rects", "boxes", "frames", "frame_boxes", "frame_rects", "tris", "spheres", "planes",
+                "groups", "grouped_slots")
+
+
+def brute_layout(prims: Sequence[rt_prim]) -> dict:
+    """rt_debug_brute_layout (host code, no GPU): how the brute-force kernels would test these
+    primitives -- world rectangles, boxes, frames, triangles, spheres, planes, and the grouping."""
+    lib = load_library()
+    n = len(prims)
+    arr = (rt_prim * max(1, n))(*prims)
+    out = (C.c_int32 * len(LAYOUT_NAMES))()
+    _check(lib.rt_debug_brute_layout(arr, n, out, len(LAYOUT_NAMES)))
+    return dict(zip(LAYOUT_NAMES, (int(v) for v in out)))
+
+
 def ref_bvh_export(prims: Sequence[rt_prim]) -> Tuple[np.ndarray, np.ndarray, int, int]:
     """The library's reference-BVH build (host code, no GPU): (leaf prim order, node boxes, nodes, depth)."""
     lib = load_library()

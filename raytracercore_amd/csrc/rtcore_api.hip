@@ -172,65 +172,9 @@ struct rt_scene {
 
 namespace {
 
-int upload_scene(rt_scene* s)
+PrimF make_primf(const std::vector<HostPrim>& H, const std::vector<int>& xf_index, int i)
 {
-    const auto& H = s->host;
-    const int n = (int)H.size();
-    // --- exact fp64 set
-    std::vector<PrimD> pd(n);
-    std::vector<XformD> xd;
-    std::vector<float4> vn((size_t)std::max(1, n) * 3, make_float4(0, 0, 0, 0));
-    std::vector<XformF> xf;
-    std::vector<int> xf_index(n, -1);
-    for (int i = 0; i < n; i++) {
-        const HostPrim& p = H[i];
-        PrimD& d = pd[i];
-        std::memset(&d, 0, sizeof d);
-        d.flags = p.flags;
-        d.xf = -1;
-        if (p.kind == RT_PRIM_TRIANGLE) {
-            d.a = p.v[0];
-            d.b = p.e01;
-            d.c = p.e02;
-            d.d = p.n;
-            for (int k = 0; k < 3; k++) {
-                d.vn[k] = p.vn[k];
-                vn[3 * i + k] = f4(p.vn[k], 0.0f);
-            }
-        } else if (p.kind == RT_PRIM_SPHERE) {
-            d.a = p.center;
-            d.b = v4d(p.radius, p.radius_sqr, 0, 0);
-            if (p.flags & F_TRANSFORMED) {
-                d.xf = (int)xd.size();
-                xf_index[i] = (int)xf.size();
-                XformD X;
-                std::memcpy(X.to_world, p.to_world, sizeof X.to_world);
-                std::memcpy(X.to_obj, p.to_obj, sizeof X.to_obj);
-                std::memcpy(X.to_normal, p.to_normal, sizeof X.to_normal);
-                xd.push_back(X);
-                XformF F;
-                const double c[3] = {p.center.x, p.center.y, p.center.z};
-                for (int r = 0; r < 3; r++) {
-                    F.to_world[r] = make_float4((float)p.to_world[4 * r], (float)p.to_world[4 * r + 1],
-                                                (float)p.to_world[4 * r + 2], (float)p.to_world[4 * r + 3]);
-                    // normal(p) = N3 * (W * p + w - c) / r: one affine map of the world hit point
-                    double row[4] = {0, 0, 0, 0};
-                    for (int k = 0; k < 3; k++) {
-                        const double nk = p.to_normal[4 * r + k] / p.radius;
-                        for (int j = 0; j < 3; j++) row[j] += nk * p.to_world[4 * k + j];
-                        row[3] += nk * (p.to_world[4 * k + 3] - c[k]);
-                    }
-                    F.normal[r] = make_float4((float)row[0], (float)row[1], (float)row[2], (float)row[3]);
-                }
-                xf.push_back(F);
-            }
-        } else {
-            d.a = p.pn;
-            d.b = v4d(p.pd, 0, 0, 0);
-        }
-    }
-    // --- fast fp32 set
-    auto primf = [&](int i) {
+    {
         const HostPrim& p = H[i];
         PrimF f;
         std::memset(&f, 0, sizeof f);
@@ -248,8 +192,11 @@ int upload_scene(rt_scene* s)
             f.d = f4(p.pn, 0.0f); // face normal where the shading step reads it for every flat kind
         }
         return f;
-    };
-    auto testrec = [&](int i) {
+    }
+}
+TestRec make_testrec(const std::vector<HostPrim>& H, const std::vector<int>& xf_index, int i)
+{
+    {
         const HostPrim& p = H[i];
         TestRec t;
         std::memset(&t, 0, sizeof t);
@@ -272,7 +219,33 @@ int upload_scene(rt_scene* s)
             t.r0 = f4(p.pn, (float)p.pd);
         }
         return t;
-    };
+    }
+}
+
+// The brute-force slot orders of a scene (flat and grouped), built on the host only: world
+// rectangles, closed and open boxes, frames, triangles, spheres and planes.
+struct BruteLayout {
+    int rects = 0, boxes = 0, frames = 0, frame_boxes = 0, frame_rects = 0, tris = 0, sphs = 0;
+};
+struct BruteOrder {
+    std::vector<PrimF> prims;
+    std::vector<TestRec> tests;
+    std::vector<RectRec> rects;
+    std::vector<FrameRec> frames; // FrameRecs and BoxRecs
+    std::vector<GroupRec> groups;
+    int nr[3] = {0, 0, 0}, nt = 0, ns = 0;
+};
+struct BruteOrders {
+    BruteOrder flat, grouped;
+    int nr[3] = {0, 0, 0}, nt = 0, ns = 0, np = 0;
+    BruteLayout layout;
+};
+BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<int>& xf_index, const SahBvh& sah)
+{
+    BruteOrders out;
+    const int n = (int)H.size();
+    auto primf = [&](int i) { return make_primf(H, xf_index, i); };
+    auto testrec = [&](int i) { return make_testrec(H, xf_index, i); };
     // An axis-aligned rectangle: a Mirror parallelogram with both edges on coordinate axes.
     auto rect_axis = [&](int i) {
         const HostPrim& p = H[i];
@@ -542,14 +515,6 @@ int upload_scene(rt_scene* s)
     // box faces | frame rects and frame box faces | triangles | spheres], then the planes.  The
     // flat order is one group of everything; the grouped order cuts the SAH BVH into subtrees of
     // at most kGroupMax primitives.
-    struct BruteOrder {
-        std::vector<PrimF> prims;
-        std::vector<TestRec> tests;
-        std::vector<RectRec> rects;
-        std::vector<FrameRec> frames; // FrameRecs and BoxRecs
-        std::vector<GroupRec> groups;
-        int nr[3] = {0, 0, 0}, nt = 0, ns = 0;
-    };
     auto fbox = [&](const std::vector<int>& ids, float lo[3], float hi[3]) {
         for (int k = 0; k < 3; k++) {
             lo[k] = __builtin_huge_valf();
@@ -710,34 +675,34 @@ int upload_scene(rt_scene* s)
     int nr[3] = {flat.nr[0], flat.nr[1], flat.nr[2]}, nt = flat.nt, ns = flat.ns, np = 0;
     if (!flat.groups.empty()) {
         const GroupRec& G = flat.groups[0];
-        s->layout.rects = G.n_rect[0] + G.n_rect[1] + G.n_rect[2];
-        s->layout.boxes = G.n_boxes;
-        s->layout.frames = G.n_frames;
-        s->layout.frame_boxes = 0;
-        s->layout.frame_rects = 0;
+        out.layout.rects = G.n_rect[0] + G.n_rect[1] + G.n_rect[2];
+        out.layout.boxes = G.n_boxes;
+        out.layout.frames = G.n_frames;
+        out.layout.frame_boxes = 0;
+        out.layout.frame_rects = 0;
         for (int f = 0; f < G.n_frames; f++) {
             const FrameRec& F = flat.frames[G.frame_first + f];
-            s->layout.frame_boxes += F.box >= 0;
-            s->layout.frame_rects += F.n_rect[0] + F.n_rect[1] + F.n_rect[2];
+            out.layout.frame_boxes += F.box >= 0;
+            out.layout.frame_rects += F.n_rect[0] + F.n_rect[1] + F.n_rect[2];
         }
-        s->layout.tris = G.n_tri_sph & 0xFFFF;
-        s->layout.sphs = G.n_tri_sph >> 16;
+        out.layout.tris = G.n_tri_sph & 0xFFFF;
+        out.layout.sphs = G.n_tri_sph >> 16;
     }
     for (int i = 0; i < n; i++) np += kind_of[i] == 5;
     // groups: subtrees of the SAH BVH with at most kGroupMax primitives (small scenes only)
     int kGroupMax = 4; // die.txt 1080p grouped: 2 -> 50.1 ms, 3 -> 47.6, 4 -> 46.4, 6 -> 48.4, 8 -> 48.4, 16 -> 50.7
     if (const char* e = getenv("RTCORE_GROUP_MAX")) kGroupMax = std::max(1, atoi(e)); // tuning
     std::vector<std::vector<int>> cut;
-    if ((int)all.size() <= 4096 && !s->sah.order.empty()) {
+    if ((int)all.size() <= 4096 && !sah.order.empty()) {
         std::function<void(int, std::vector<int>&)> leaves = [&](int ref, std::vector<int>& out) {
             if (ref < 0) {
                 const int code = ~ref, first = code >> 3, c = (code & 7) + 1;
-                for (int k = first; k < first + c; k++) out.push_back(s->sah.order[k]);
+                for (int k = first; k < first + c; k++) out.push_back(sah.order[k]);
                 return;
             }
             int l, r;
-            std::memcpy(&l, &s->sah.nodes[ref].lmin.w, 4);
-            std::memcpy(&r, &s->sah.nodes[ref].rmin.w, 4);
+            std::memcpy(&l, &sah.nodes[ref].lmin.w, 4);
+            std::memcpy(&r, &sah.nodes[ref].rmin.w, 4);
             leaves(l, out);
             leaves(r, out);
         };
@@ -749,14 +714,97 @@ int upload_scene(rt_scene* s)
                 return;
             }
             int l, r;
-            std::memcpy(&l, &s->sah.nodes[ref].lmin.w, 4);
-            std::memcpy(&r, &s->sah.nodes[ref].rmin.w, 4);
+            std::memcpy(&l, &sah.nodes[ref].lmin.w, 4);
+            std::memcpy(&r, &sah.nodes[ref].rmin.w, 4);
             split(l);
             split(r);
         };
-        split(s->sah.root);
+        split(sah.root);
     }
     BruteOrder grouped = cut.empty() ? BruteOrder{} : build_order(cut);
+    out.flat = std::move(flat);
+    out.grouped = std::move(grouped);
+    for (int k = 0; k < 3; k++) out.nr[k] = nr[k];
+    out.nt = nt;
+    out.ns = ns;
+    out.np = np;
+    return out;
+}
+
+int upload_scene(rt_scene* s)
+{
+    const auto& H = s->host;
+    const int n = (int)H.size();
+    // --- exact fp64 set
+    std::vector<PrimD> pd(n);
+    std::vector<XformD> xd;
+    std::vector<float4> vn((size_t)std::max(1, n) * 3, make_float4(0, 0, 0, 0));
+    std::vector<XformF> xf;
+    std::vector<int> xf_index(n, -1);
+    for (int i = 0; i < n; i++) {
+        const HostPrim& p = H[i];
+        PrimD& d = pd[i];
+        std::memset(&d, 0, sizeof d);
+        d.flags = p.flags;
+        d.xf = -1;
+        if (p.kind == RT_PRIM_TRIANGLE) {
+            d.a = p.v[0];
+            d.b = p.e01;
+            d.c = p.e02;
+            d.d = p.n;
+            for (int k = 0; k < 3; k++) {
+                d.vn[k] = p.vn[k];
+                vn[3 * i + k] = f4(p.vn[k], 0.0f);
+            }
+        } else if (p.kind == RT_PRIM_SPHERE) {
+            d.a = p.center;
+            d.b = v4d(p.radius, p.radius_sqr, 0, 0);
+            if (p.flags & F_TRANSFORMED) {
+                d.xf = (int)xd.size();
+                xf_index[i] = (int)xf.size();
+                XformD X;
+                std::memcpy(X.to_world, p.to_world, sizeof X.to_world);
+                std::memcpy(X.to_obj, p.to_obj, sizeof X.to_obj);
+                std::memcpy(X.to_normal, p.to_normal, sizeof X.to_normal);
+                xd.push_back(X);
+                XformF F;
+                const double c[3] = {p.center.x, p.center.y, p.center.z};
+                for (int r = 0; r < 3; r++) {
+                    F.to_world[r] = make_float4((float)p.to_world[4 * r], (float)p.to_world[4 * r + 1],
+                                                (float)p.to_world[4 * r + 2], (float)p.to_world[4 * r + 3]);
+                    // normal(p) = N3 * (W * p + w - c) / r: one affine map of the world hit point
+                    double row[4] = {0, 0, 0, 0};
+                    for (int k = 0; k < 3; k++) {
+                        const double nk = p.to_normal[4 * r + k] / p.radius;
+                        for (int j = 0; j < 3; j++) row[j] += nk * p.to_world[4 * k + j];
+                        row[3] += nk * (p.to_world[4 * k + 3] - c[k]);
+                    }
+                    F.normal[r] = make_float4((float)row[0], (float)row[1], (float)row[2], (float)row[3]);
+                }
+                xf.push_back(F);
+            }
+        } else {
+            d.a = p.pn;
+            d.b = v4d(p.pd, 0, 0, 0);
+        }
+    }
+    // --- fast fp32 set
+    auto primf = [&](int i) { return make_primf(H, xf_index, i); };
+    auto testrec = [&](int i) { return make_testrec(H, xf_index, i); };
+    BruteOrders orders = make_brute_orders(H, xf_index, s->sah);
+    BruteOrder& flat = orders.flat;
+    BruteOrder& grouped = orders.grouped;
+    int nr[3] = {orders.nr[0], orders.nr[1], orders.nr[2]}, nt = orders.nt, ns = orders.ns, np = orders.np;
+    {
+        const BruteLayout& L = orders.layout;
+        s->layout.rects = L.rects;
+        s->layout.boxes = L.boxes;
+        s->layout.frames = L.frames;
+        s->layout.frame_boxes = L.frame_boxes;
+        s->layout.frame_rects = L.frame_rects;
+        s->layout.tris = L.tris;
+        s->layout.sphs = L.sphs;
+    }
     std::vector<PrimF> bv;
     std::vector<TestRec> tbv;
     size_t n_bvh_records = 0;
@@ -1212,6 +1260,36 @@ int rt_set_bvh_builder(int32_t builder)
         return RT_ERR_ARG;
     }
     g_builder.store(builder);
+    return RT_OK;
+}
+
+int rt_debug_brute_layout(const rt_prim* prims, int32_t n_prims, int32_t* out, int32_t n_out)
+{
+    if (n_prims < 0 || (n_prims > 0 && !prims) || !out || n_out < 0) {
+        set_error("rt_debug_brute_layout: bad argument");
+        return RT_ERR_ARG;
+    }
+    for (int i = 0; i < n_prims; i++)
+        if (prims[i].kind < 0 || prims[i].kind > 2) {
+            set_error("rt_debug_brute_layout: unknown primitive kind at index " + std::to_string(i));
+            return RT_ERR_ARG;
+        }
+    const std::vector<HostPrim> H = prepare_prims(prims, n_prims);
+    const int n = (int)H.size();
+    std::vector<int> xf_index(n, -1);
+    int nb = 0, nx = 0;
+    for (int i = 0; i < n; i++) {
+        nb += H[i].kind != RT_PRIM_PLANE;
+        if (H[i].kind == RT_PRIM_SPHERE && (H[i].flags & F_TRANSFORMED)) xf_index[i] = nx++;
+    }
+    SahBvh sah; // the grouping cuts the host SAH tree, as rt_scene_create does for small scenes
+    if (nb > 0 && builder_for(nb) == RT_BVH_BUILDER_HOST) sah = build_sah_bvh(H, n > 256 ? 4 : 2);
+    const BruteOrders o = make_brute_orders(H, xf_index, sah);
+    const BruteLayout& L = o.layout;
+    const int32_t v[RT_LAYOUT_COUNT] = {L.rects, L.boxes, L.frames, L.frame_boxes, L.frame_rects, L.tris, L.sphs,
+                                        o.np, o.grouped.groups.empty() ? 0 : (int32_t)o.grouped.groups.size(),
+                                        (int32_t)o.grouped.prims.size() - o.np};
+    for (int i = 0; i < n_out && i < RT_LAYOUT_COUNT; i++) out[i] = v[i];
     return RT_OK;
 }
 

@@ -195,3 +195,42 @@ def test_wide_bvh_structure(rc, bvh_check_bin, tmp_path, name):
     path.write_text(text)
     out = subprocess.run([bvh_check_bin, str(path)], capture_output=True, text=True)
     assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
+
+
+# --- brute-force layout (host code): rectangles, boxes and frames --------------------------
+
+def _layout(rc, text):
+    return rc.brute_layout(list(rc.SceneLoader.from_text(text).prims))
+
+
+def test_brute_layout_shipped_scenes(rc):
+    """bounce.txt: the inverted room and the open light box are world boxes, the rotated cube a
+    frame box, the cut-out corner two single rectangles; die.txt: the die is one box."""
+    b = rc.brute_layout(list(rc.SceneLoader.from_file(rc.scene_path("bounce.txt")).prims))
+    assert (b["rects"], b["boxes"], b["frames"], b["frame_boxes"], b["frame_rects"], b["tris"], b["spheres"]) == \
+        (2, 2, 1, 1, 0, 0, 3)
+    d = rc.brute_layout(list(rc.SceneLoader.from_file(rc.scene_path("die.txt")).prims))
+    assert (d["rects"], d["boxes"], d["frames"], d["tris"], d["spheres"]) == (0, 1, 0, 0, 23)
+    assert d["groups"] > 1 and d["grouped_slots"] >= 29
+
+
+HEAD = "size 16 12\ncamera 0 -6 1, 0 0 0, 0 0 1, 60\n"
+
+
+@pytest.mark.parametrize("text,expect", [
+    ("cube 0 0 0 1 1 1 all\n", dict(boxes=1, rects=0)),                     # closed box
+    ("cube 0 0 0 1 2 3 not -z\n", dict(boxes=1, rects=0)),                  # open box (5 faces)
+    ("cube 0 0 0 1 1 1 only +x -x +y -y\n", dict(boxes=0, rects=4)),       # 4 faces: rectangles
+    ("cube 0 0 0 1 1 1 only +x -y\n", dict(boxes=0, rects=2)),
+    ("cube 0 0 0 1 1 1 all\ncube 3 0 0 1 1 1 all\n", dict(boxes=2, rects=0)),
+    ("pushtransform\nrotate 1 2 3 30\ncube 0 0 0 1 2 3 all\npoptransform\n",
+     dict(boxes=0, rects=0, frames=1, frame_boxes=1, frame_rects=0)),      # box in a rotated frame
+    ("pushtransform\nrotate 0 0 1 30\ncube 0 0 0 1 1 1 only +x -x +y\npoptransform\n",
+     dict(frames=1, frame_boxes=0, frame_rects=3)),                        # frame, too few faces for a box
+    ("pushtransform\nrotate 0 0 1 30\ncube 0 0 0 1 1 1 only +x\npoptransform\n",
+     dict(frames=0, tris=1)),                                              # a lone parallelogram stays a triangle
+    ("plane 3 0 1 0\ncube 0 0 0 1 1 1 not -z\n", dict(boxes=1, planes=1)),
+])
+def test_brute_layout_detection(rc, text, expect):
+    got = _layout(rc, HEAD + text)
+    assert {k: got[k] for k in expect} == expect
