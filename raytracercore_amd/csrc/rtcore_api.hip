@@ -126,6 +126,7 @@ struct rt_scene {
     DevBuf<RectRec> rects_gr;
     DevBuf<FrameRec> frames_gr;
     DevBuf<GroupRec> groups_gr;
+    std::vector<GroupRec> groups_gr_host; // in build order; uploaded nearest-first per camera
     double grouped_measured = 0; // calibrated brute-force cost ratio flat / grouped (AUTO picks grouped above 1.25)
     DevBuf<NodeF> nodes;
     DevBuf<Node4Q> nodes4;
@@ -879,6 +880,7 @@ int upload_scene(rt_scene* s)
     HIP_TRY(s->rects_gr.upload(grouped.rects));
     HIP_TRY(s->frames_gr.upload(grouped.frames));
     HIP_TRY(s->groups_gr.upload(grouped.groups));
+    s->groups_gr_host = grouped.groups;
     if (s->bvh.builder != RT_BVH_BUILDER_GPU) {
         HIP_TRY(s->prims_bvh.upload(bv));
         tbv.push_back(TestRec{}); // spare record: the BVH leaf step loads one past a leaf
@@ -1560,6 +1562,22 @@ int rt_scene_set_camera(rt_scene* s, const rt_camera* cam)
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(s->camf_d.reserve(1));
     HIP_TRY(hipMemcpy(s->camf_d.p, &s->camf, sizeof(CameraF), hipMemcpyHostToDevice));
+    // The grouped order's groups nearest to the camera first: camera rays find their closest hit
+    // early and skip the primitives of groups behind it (each group owns its own ranges, so only
+    // the GroupRec order changes).  Deterministic for a given scene and camera.
+    if (s->groups_gr_host.size() > 1 && !getenv("RTCORE_NO_GROUP_SORT")) {
+        std::vector<GroupRec> g = s->groups_gr_host;
+        const double px = s->camd.position.x, py = s->camd.position.y, pz = s->camd.position.z;
+        auto dist2 = [&](const GroupRec& G) {
+            // distance from the camera to the group's box (0 inside)
+            const double dx = std::max({0.0, (double)G.lo.x - px, px - (double)G.hi.x});
+            const double dy = std::max({0.0, (double)G.lo.y - py, py - (double)G.hi.y});
+            const double dz = std::max({0.0, (double)G.lo.z - pz, pz - (double)G.hi.z});
+            return dx * dx + dy * dy + dz * dz;
+        };
+        std::stable_sort(g.begin(), g.end(), [&](const GroupRec& a, const GroupRec& b) { return dist2(a) < dist2(b); });
+        HIP_TRY(hipMemcpy(s->groups_gr.p, g.data(), g.size() * sizeof(GroupRec), hipMemcpyHostToDevice));
+    }
     s->has_camera = true;
     return calibrate_grouping(s);
 }
