@@ -5,7 +5,7 @@ import subprocess
 import sys
 
 extra = sys.argv[1:]
-cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950", "-x", "hip", "-c",
+cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "--offload-arch=gfx950", "-x", "hip", "-c",
        "raytracercore_amd/csrc/kernels_path.hip", "-o", "/dev/null", "-Rpass-analysis=kernel-resource-usage"] + extra
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 cur = None
