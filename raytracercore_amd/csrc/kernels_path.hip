@@ -660,6 +660,9 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
 #ifndef RT_WIDE_STACK
 #define RT_WIDE_STACK 24 // LDS entries of the wide BVH kernel's traversal stack (then global overflow)
 #endif
+#ifndef RT_BVH_SPEC
+#define RT_BVH_SPEC 1 // speculative BVH traversal with wave-wide leaf steps (p.spec); 0: the mixed-step loop (C4 69.8 -> 62.1 ms)
+#endif
 #ifndef RT_LEAF_STEP
 #define RT_LEAF_STEP 2 // leaf primitives tested per BVH traversal step
 #endif
@@ -932,11 +935,13 @@ __global__ void __launch_bounds__(256, CULL ? RT_GROUPED_WAVES : RT_PATH_WAVES)
     flush_counts<STATS>(wave_rays, cnt, *pp, lane);
 }
 
-// BVH megakernel with decoupled traversal.  A loop iteration advances every traversing lane by
-// one step (one node visit, or one leaf's primitives); lanes whose query finished wait, and
-// the shading / new-sample phase runs only once at least p.refill lanes wait (or none is still
-// traversing).  So one long traversal no longer holds the other 63 lanes of its wave, and the
-// divergent shading code is paid once per batch of finished queries.
+// BVH megakernel with decoupled traversal.  A loop iteration advances the traversing lanes by
+// one step: with RT_BVH_SPEC a wave-wide node step or leaf step (up to two primitives), lanes
+// keeping a reached leaf pending while they visit further nodes; without it, one node visit or
+// one leaf step per lane.  Lanes whose query finished wait, and the shading / new-sample phase
+// runs only once at least p.refill lanes wait (or none is still traversing).  So one long
+// traversal no longer holds the other 63 lanes of its wave, and the divergent shading code is
+// paid once per batch of finished queries.
 template <int WIDTH, int STACK, bool LDS, bool STATS>
 __global__ void __launch_bounds__(256, RT_BVH_WAVES)
     path_kernel_bvh(PathScene s, const CameraF* __restrict__ camp, const PathParams* __restrict__ pp,
@@ -973,6 +978,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
     unsigned long long wave_rays = 0; // wave-uniform
     // traversal state of the lane's current query
     bool trav = false, done = false;
+    [[maybe_unused]] bool more = false; // RT_BVH_SPEC: ref still holds a reference to process (stack not exhausted)
     int ref = 0, sp = 0, k = 0, kend = 0; // [k, kend): primitives of the leaf being tested
     V3 id{0, 0, 0}, oi{0, 0, 0}; // 1/d and o/d of the query
     Best b{__builtin_huge_valf(), -1};
@@ -995,14 +1001,86 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                 ref = s.root;
                 sp = 0;
                 k = kend = 0;
+                more = true;
                 if (ref < 0) { // the root itself is a leaf
                     k = (~ref) >> 3;
                     kend = k + ((~ref) & 7) + 1;
+                    more = false;
                 }
                 b = Best{__builtin_huge_valf(), -1};
                 trav = true;
             }
         }
+#if RT_BVH_SPEC
+        // Speculative traversal (Aila & Laine 2009): a lane that reaches a leaf keeps it pending and
+        // goes on visiting nodes.  Leaf primitives are tested in wave-wide leaf steps, taken once
+        // p.spec lanes are blocked (a second leaf reached, or no node left) or no lane can visit a
+        // node, so an iteration is one kind of step instead of both.  Node culling uses the best hit
+        // so far (the pending leaf not yet tested): more visits, the same closest hit.
+        const bool can_node = trav && more && ref >= 0;
+        const bool blocked = trav && k < kend && !can_node;
+        const bool leaf_step = __ballot(can_node) == 0 || __popcll(__ballot(blocked)) >= p.spec; // wave-uniform
+        if (trav) {
+            if (leaf_step) {
+                if (k < kend) {
+                    const TestRec r0 = tests[k];
+                    const TestRec r1 = tests[k + 1]; // the record array carries a spare at the end
+                    if (STATS) {
+                        if ((__float_as_uint(r0.meta.y) & KIND_MASK) == RT_PRIM_TRIANGLE) cnt.tris++;
+                        else cnt.sphs++;
+                    }
+                    hit_any(r0, k, S.o, S.d, S.prev, xf, b);
+                    if (k + 1 < kend) {
+                        if (STATS) {
+                            if ((__float_as_uint(r1.meta.y) & KIND_MASK) == RT_PRIM_TRIANGLE) cnt.tris++;
+                            else cnt.sphs++;
+                        }
+                        hit_any(r1, k + 1, S.o, S.d, S.prev, xf, b);
+                    }
+                    k += 2;
+                }
+            } else if (can_node) {
+                bool pop = true;
+                if (WIDTH == 4) {
+                    const Node4Q q = (ref & RT_HOT_BIT) ? lds_hot[ref & ~RT_HOT_BIT] : nodes4[ref];
+                    wide_visit<STACK>(q, id, oi, b.t, ref, sp, stk, pop);
+                } else {
+                    const NodeF n = nodes[ref];
+                    float tl, tr;
+                    const bool hl = slab(n.lmin, n.lmax, oi, id, b.t, tl);
+                    const bool hr = slab(n.rmin, n.rmax, oi, id, b.t, tr);
+                    const int cl = __float_as_int(n.lmin.w), cr = __float_as_int(n.rmin.w);
+                    if (hl && hr) {
+                        const bool lf = tl <= tr;
+                        push<STACK>(stk, sp, lf ? cr : cl);
+                        ref = lf ? cl : cr;
+                        pop = false;
+                    } else if (hl | hr) {
+                        ref = hl ? cl : cr;
+                        pop = false;
+                    }
+                }
+                if (STATS) cnt.nodes++;
+                if (pop) {
+                    if (sp > 0) ref = pop_ref<STACK>(stk, sp);
+                    else more = false;
+                }
+            }
+            // a leaf reference becomes the pending leaf once the previous one is tested, and the
+            // next reference is popped so that traversal goes on past it
+            if (more && ref < 0 && k >= kend) {
+                const int code = ~ref;
+                k = code >> 3;
+                kend = k + (code & 7) + 1;
+                if (sp > 0) ref = pop_ref<STACK>(stk, sp);
+                else more = false;
+            }
+            if (!more && k >= kend) {
+                trav = false;
+                done = true;
+            }
+        }
+#else
         if (trav) { // one traversal step: one node visit, or one primitive of the current leaf
             bool pop = true; // child references are node indices or ~leaf codes (any int)
             if (k < kend) { // up to RT_LEAF_STEP primitives, their loads issued together
@@ -1062,6 +1140,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                 kend = k + (code & 7) + 1;
             }
         }
+#endif
         if (STATS) {
             cnt.iters++;
             if (trav) cnt.q_steps++;

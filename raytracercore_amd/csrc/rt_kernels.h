@@ -17,6 +17,7 @@ struct PathParams {
     int blocks_x;               // 8x8 pixel blocks per tile row
     int n_pad;                  // padded pixels per chunk (blocks * 64)
     int refill;                 // BVH kernel: waiting lanes (of 64) that trigger the shading phase
+    int spec;                   // BVH kernel (RT_BVH_SPEC): lanes blocked on a pending leaf that trigger a leaf step
     int pool;                   // work items a wave takes per atomic: 64 x a power of two <= n_chunks
                                 // (all from one 8x8 block, so a wave's lanes stay on neighbouring pixels)
     float inv_blocks_x;         // fp32 reciprocal for the item decode

@@ -1127,8 +1127,14 @@ PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint6
     if (const char* e = getenv("RTCORE_POOL_MUL")) pool_mul = std::max(1, std::min(64, atoi(e)));
     p.pool = 64;
     while (p.pool < 64 * pool_mul && p.pool < 64 * p.n_chunks) p.pool *= 2;
-    p.refill = 16;
+    // BVH kernels: the shading phase runs once 24 lanes wait (C4 with speculative traversal:
+    // 8 / 16 / 20 / 24 / 28 / 32 lanes: 71.8 / 64.3 / 63.2 / 62.1-62.6 / 62.9 / 63.6 ms); a leaf step
+    // once 16 lanes are blocked on a pending leaf (12 / 16 / 20 / 24 / 32 / 48: 64.8 / 64.3 / 63.6 /
+    // 65.3 / 68.1 / 89.5 ms at refill 16)
+    p.refill = 24;
     if (const char* e = getenv("RTCORE_BVH_REFILL")) p.refill = std::max(1, std::min(64, atoi(e)));
+    p.spec = 16;
+    if (const char* e = getenv("RTCORE_BVH_SPEC")) p.spec = std::max(1, std::min(64, atoi(e)));
     p.seed = seed;
     p.seed_key = rt_rng_seed_key(seed);
     p.sample_base = base;
