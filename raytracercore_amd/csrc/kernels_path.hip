@@ -663,6 +663,9 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
 #ifndef RT_BVH_SPEC
 #define RT_BVH_SPEC 1 // speculative BVH traversal with wave-wide leaf steps (p.spec); 0: the mixed-step loop (C4 69.8 -> 62.1 ms)
 #endif
+#ifndef RT_SPEC_PRIMS
+#define RT_SPEC_PRIMS 2 // leaf primitives per leaf step of the speculative traversal (<= kTestSpares + 1)
+#endif
 #ifndef RT_LEAF_STEP
 #define RT_LEAF_STEP 2 // leaf primitives tested per BVH traversal step
 #endif
@@ -1022,22 +1025,21 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
         const bool leaf_step = __ballot(can_node) == 0 || __popcll(__ballot(blocked)) >= p.spec; // wave-uniform
         if (trav) {
             if (leaf_step) {
-                if (k < kend) {
-                    const TestRec r0 = tests[k];
-                    const TestRec r1 = tests[k + 1]; // the record array carries a spare at the end
-                    if (STATS) {
-                        if ((__float_as_uint(r0.meta.y) & KIND_MASK) == RT_PRIM_TRIANGLE) cnt.tris++;
-                        else cnt.sphs++;
-                    }
-                    hit_any(r0, k, S.o, S.d, S.prev, xf, b);
-                    if (k + 1 < kend) {
-                        if (STATS) {
-                            if ((__float_as_uint(r1.meta.y) & KIND_MASK) == RT_PRIM_TRIANGLE) cnt.tris++;
-                            else cnt.sphs++;
+                if (k < kend) { // RT_SPEC_PRIMS primitives of the pending leaf, their loads issued together
+                    TestRec r[RT_SPEC_PRIMS];
+#pragma unroll
+                    for (int j = 0; j < RT_SPEC_PRIMS; j++) r[j] = tests[k + j]; // kTestSpares zero records follow the last leaf
+#pragma unroll
+                    for (int j = 0; j < RT_SPEC_PRIMS; j++) {
+                        if (j == 0 || k + j < kend) {
+                            if (STATS) {
+                                if ((__float_as_uint(r[j].meta.y) & KIND_MASK) == RT_PRIM_TRIANGLE) cnt.tris++;
+                                else cnt.sphs++;
+                            }
+                            hit_any(r[j], k + j, S.o, S.d, S.prev, xf, b);
                         }
-                        hit_any(r1, k + 1, S.o, S.d, S.prev, xf, b);
                     }
-                    k += 2;
+                    k += RT_SPEC_PRIMS;
                 }
             } else if (can_node) {
                 bool pop = true;

@@ -41,6 +41,7 @@ hipError_t launch_primary_ids(const DevScene& s, const CameraD& cam, int x0, int
 // lds stages the shading records in LDS.
 int path_variant(int kernel, bool lds);
 constexpr int kStackOverflow = 40; // = RT_STACK_OVF (kernels_path.hip)
+constexpr int kTestSpares = 3;     // zero TestRecs after the BVH-order records (leaf steps of up to 4 loads)
 int path_wide_stack();              // LDS entries of the wide BVH kernel's stack (RT_WIDE_STACK)
 size_t path_lds_bytes(const DevScene& s);   // dynamic LDS of the staged (lds) variants
 size_t path_dyn_lds(const DevScene& s, int variant); // all dynamic LDS of a variant (+ the wide kernel's hot nodes)

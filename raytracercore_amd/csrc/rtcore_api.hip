@@ -829,11 +829,11 @@ int upload_scene(rt_scene* s)
         HIP_TRY(pid_d.upload(pid));
         HIP_TRY(tid_d.upload(tid));
         HIP_TRY(s->prims_bvh.reserve(n_bvh_records));
-        HIP_TRY(s->tests_bvh.reserve(n_bvh_records + 1));
+        HIP_TRY(s->tests_bvh.reserve(n_bvh_records + kTestSpares));
         HIP_TRY(gather_bvh_records(s->order_d.p, (int)n_bvh_records, pid_d.p, tid_d.p, s->prims_bvh.p, s->tests_bvh.p,
                                    s->stream));
-        // spare record: the BVH leaf step loads one past a leaf
-        HIP_TRY(hipMemsetAsync(s->tests_bvh.p + n_bvh_records, 0, sizeof(TestRec), s->stream));
+        // spare records: the BVH leaf step loads up to kTestSpares past a leaf
+        HIP_TRY(hipMemsetAsync(s->tests_bvh.p + n_bvh_records, 0, kTestSpares * sizeof(TestRec), s->stream));
         HIP_TRY(hipStreamSynchronize(s->stream));
         s->order_d.release();
     } else {
@@ -883,7 +883,7 @@ int upload_scene(rt_scene* s)
     s->groups_gr_host = grouped.groups;
     if (s->bvh.builder != RT_BVH_BUILDER_GPU) {
         HIP_TRY(s->prims_bvh.upload(bv));
-        tbv.push_back(TestRec{}); // spare record: the BVH leaf step loads one past a leaf
+        tbv.resize(tbv.size() + kTestSpares, TestRec{}); // spare records: the BVH leaf step loads past a leaf
         HIP_TRY(s->tests_bvh.upload(tbv));
         HIP_TRY(s->nodes.upload(s->sah.nodes));
         HIP_TRY(s->nodes4.upload(s->bvh4.nodes));
