@@ -20,7 +20,11 @@
  *     as in Raytracer.cs:305,317 and FullRaytracer.cs:328-339.
  *   - The library owns scene handles and device memory; callers own every output
  *     buffer and nothing is retained after a call returns.
- *   - A scene handle is bound to one device and is not re-entrant.
+ *   - A scene handle is bound to one device and is not re-entrant: calls on one handle
+ *     are serialised by the caller.  Device-side calls may be queued on any stream; the
+ *     library orders an operation on a stream other than the previous one after it
+ *     (the launches share per-scene scratch), and any number of launches may be queued
+ *     without a synchronisation.
  */
 #ifndef RTCORE_H
 #define RTCORE_H
@@ -32,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RTCORE_ABI_VERSION 1
+#define RTCORE_ABI_VERSION 2 /* 2: rt_frame_*, rt_render_bands, sample_base in rt_render_frame_multi */
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -260,14 +264,41 @@ int rt_scene_get_stats(rt_scene* scene, uint64_t* out, int32_t n);
 
 /* ------------------------------------------------------------- multi-GPU ---- */
 /*
- * Whole frame on n_gpus devices of this process: rows are dealt to devices in
- * interleaved 16-row bands, each device renders its bands, and an RCCL gather over xGMI
- * assembles the accumulators on device 0, which are copied to the caller's buffers in
- * the frame's x*height + y order.
+ * Row bands.  A band set (band, stride, offset) is the frame rows y with
+ * (y / band) % stride == offset.  rt_frame deals the rows of a frame to n devices as the sets
+ * (16, n, g), g = 0..n-1: interleaved bands balance background-heavy rows, where the
+ * reference's contiguous tiles (FullRaytracer.cs:71-72) would not.
+ *
+ * rt_render_bands renders one band set on one scene and adds it into whole-frame buffers
+ * (x*height + y order, every row outside the set untouched): the per-device step of
+ * rt_frame_render, with the same device layout, callable on one device.
  */
+int rt_render_bands(rt_scene* scene, int32_t band, int32_t band_stride, int32_t band_offset, int32_t spp,
+                    uint64_t seed, uint64_t sample_base, rt_color* sum_rgb, uint32_t* samples,
+                    uint32_t* misses, uint64_t* rays_out);
+
+/*
+ * Persistent whole-frame renderer over devices 0..n_gpus-1 of this process (replaces the
+ * FullRaytracer worker pool, FullRaytracer.cs:297-302, for a multi-GPU host): one scene per
+ * device and one RCCL communicator, created once.  Each rt_frame_render call renders spp
+ * samples (indices sample_base .. sample_base+spp-1) of every pixel: each device its band set,
+ * then one RCCL gather over xGMI to device 0, and adds the result into the caller's frame
+ * buffers (x*height + y; SampleSet semantics as rt_render_tile).  Progressive callers pass
+ * disjoint sample_base ranges with the same seed.
+ */
+typedef struct rt_frame rt_frame; /* opaque */
+int rt_frame_create(const rt_scene_params* params, const rt_prim* prims, int32_t n_prims,
+                    const rt_camera* camera, int32_t n_gpus, rt_frame** out_frame);
+int rt_frame_set_camera(rt_frame* frame, const rt_camera* camera);
+int rt_frame_render(rt_frame* frame, int32_t spp, uint64_t seed, uint64_t sample_base,
+                    rt_color* sum_rgb, uint32_t* samples, uint32_t* misses, uint64_t* rays_out);
+void rt_frame_destroy(rt_frame* frame);
+
+/* One-shot rt_frame_create + rt_frame_render + rt_frame_destroy. */
 int rt_render_frame_multi(const rt_scene_params* params, const rt_prim* prims, int32_t n_prims,
                           const rt_camera* camera, int32_t n_gpus, int32_t spp, uint64_t seed,
-                          rt_color* sum_rgb, uint32_t* samples, uint32_t* misses, uint64_t* rays_out);
+                          uint64_t sample_base, rt_color* sum_rgb, uint32_t* samples, uint32_t* misses,
+                          uint64_t* rays_out);
 
 /* ------------------------------------------------------------- scene text ---- */
 /*

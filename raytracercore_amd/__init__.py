@@ -23,6 +23,7 @@ LIB_PATH = os.path.join(_HERE, "librtcore_hip.so")
 REPO_ROOT = os.path.dirname(_HERE)
 
 RT_OK = 0
+ABI_VERSION = 2  # RTCORE_ABI_VERSION of include/rtcore.h
 RT_PRIM_TRIANGLE, RT_PRIM_SPHERE, RT_PRIM_PLANE = 0, 1, 2
 RT_FLAG_MIRROR, RT_FLAG_TWOSIDED, RT_FLAG_INVERT, RT_FLAG_HASNORMALS, RT_FLAG_TRANSFORMED = 1, 2, 4, 8, 16
 RT_CAMERA_FRUSTUM, RT_CAMERA_ORTHO = 0, 1
@@ -126,8 +127,16 @@ def load_library(path: str = "") -> C.CDLL:
         "rt_scene_set_stats": (C.c_int, [C.c_void_p, C.c_int32]),
         "rt_scene_get_stats": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_int32]),
         "rt_render_frame_multi": (C.c_int, [P(rt_scene_params), P(rt_prim), C.c_int32, P(rt_camera), C.c_int32,
-                                            C.c_int32, C.c_uint64, P(rt_color), P(C.c_uint32), P(C.c_uint32),
-                                            P(C.c_uint64)]),
+                                            C.c_int32, C.c_uint64, C.c_uint64, P(rt_color), P(C.c_uint32),
+                                            P(C.c_uint32), P(C.c_uint64)]),
+        "rt_render_bands": (C.c_int, [C.c_void_p] + [C.c_int32] * 4 + [C.c_uint64, C.c_uint64, P(rt_color),
+                                      P(C.c_uint32), P(C.c_uint32), P(C.c_uint64)]),
+        "rt_frame_create": (C.c_int, [P(rt_scene_params), P(rt_prim), C.c_int32, P(rt_camera), C.c_int32,
+                                      P(C.c_void_p)]),
+        "rt_frame_set_camera": (C.c_int, [C.c_void_p, P(rt_camera)]),
+        "rt_frame_render": (C.c_int, [C.c_void_p, C.c_int32, C.c_uint64, C.c_uint64, P(rt_color), P(C.c_uint32),
+                                      P(C.c_uint32), P(C.c_uint64)]),
+        "rt_frame_destroy": (None, [C.c_void_p]),
         "rt_parse_scene": (C.c_int, [C.c_char_p, P(rt_scene_params), P(rt_prim), P(C.c_int32), P(rt_camera),
                                      P(C.c_int32)]),
         "rt_sample_output": (C.c_int32, [rt_color, C.c_uint32, C.c_uint32, rt_color, C.c_double, C.c_double]),
@@ -140,6 +149,8 @@ def load_library(path: str = "") -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.rt_abi_version() != ABI_VERSION:
+        raise RtError(f"{path}: ABI version {lib.rt_abi_version()}, this module binds {ABI_VERSION} (rebuild)")
     _lib = lib
     return lib
 
@@ -312,6 +323,20 @@ class GpuRaytracer:
                                        m.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(rays)))
         return s, n, m, rays.value
 
+    def render_bands(self, band: int, band_stride: int, band_offset: int, spp: int, seed: int = 0,
+                     sample_base: int = 0, out=None):
+        """rt_render_bands: one band set of the frame added into whole-frame accumulators
+        (sum[W,H,3] f64, samples[W,H] u32, misses[W,H] u32; new zeroed arrays unless `out`), plus rays."""
+        W, H = self.width, self.height
+        if out is None:
+            out = (np.zeros((W, H, 3), np.float64), np.zeros((W, H), np.uint32), np.zeros((W, H), np.uint32))
+        s, n, m = out
+        rays = C.c_uint64(0)
+        _check(self.lib.rt_render_bands(self.handle, band, band_stride, band_offset, spp, seed, sample_base,
+                                        s.ctypes.data_as(C.POINTER(rt_color)), n.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                        m.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(rays)))
+        return s, n, m, rays.value
+
     def render_tile_1spp(self, x0: int, y0: int, w: int, h: int, seed: int = 0, sample_index: int = 0) -> np.ndarray:
         """Raytracer.Render one pass: DoubleColor[w, h] with Placeholder (-1) for misses."""
         out = np.empty((w, h, 3), np.float64)
@@ -353,23 +378,70 @@ def tonemap_device(d_sum: int, d_samples: int, d_misses: int, w: int, h: int, d_
                                             background_alpha, exposure, d_argb, stream))
 
 
-def render_frame_multi(scene: ParsedScene, camera_index: int, n_gpus: int, spp: int, seed: int = 0,
-                       size: Optional[Tuple[int, int]] = None):
-    """rt_render_frame_multi: row-interleaved bands on n_gpus devices + RCCL gather."""
-    lib = load_library()
+def _frame_inputs(scene: ParsedScene, camera_index: int, size: Optional[Tuple[int, int]]):
     params = rt_scene_params.from_buffer_copy(scene.params)
     if size is not None:
         params.width, params.height = size
+    prims = (rt_prim * max(1, scene.n_prims))(*scene.prims)
+    cam = rt_camera.from_buffer_copy(scene.cameras[camera_index])
+    return params, prims, cam
+
+
+class GpuFrame:
+    """rt_frame: persistent whole-frame renderer over devices 0..n_gpus-1 of this process (row-band
+    split, one RCCL gather to device 0 per render).  Replaces FullRaytracer's worker pool
+    (FullRaytracer.cs:297-302) on a multi-GPU host; accumulators in the [x, y] order of SampleSet[w, h]."""
+
+    def __init__(self, scene: ParsedScene, camera_index: int = 0, n_gpus: int = 1,
+                 size: Optional[Tuple[int, int]] = None):
+        self.lib = load_library()
+        params, prims, cam = _frame_inputs(scene, camera_index, size)
+        self.width, self.height = params.width, params.height
+        self.handle = C.c_void_p()
+        _check(self.lib.rt_frame_create(C.byref(params), prims, scene.n_prims, C.byref(cam), n_gpus,
+                                        C.byref(self.handle)))
+
+    def set_camera(self, camera: rt_camera) -> None:
+        _check(self.lib.rt_frame_set_camera(self.handle, C.byref(camera)))
+
+    def render(self, spp: int, seed: int = 0, sample_base: int = 0, out=None):
+        """Adds spp samples of every pixel into (sum[W,H,3], samples[W,H], misses[W,H]) (new if out is None)."""
+        W, H = self.width, self.height
+        if out is None:
+            out = (np.zeros((W, H, 3), np.float64), np.zeros((W, H), np.uint32), np.zeros((W, H), np.uint32))
+        s, n, m = out
+        rays = C.c_uint64(0)
+        _check(self.lib.rt_frame_render(self.handle, spp, seed, sample_base, s.ctypes.data_as(C.POINTER(rt_color)),
+                                        n.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                        m.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(rays)))
+        return s, n, m, rays.value
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.rt_frame_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def render_frame_multi(scene: ParsedScene, camera_index: int, n_gpus: int, spp: int, seed: int = 0,
+                       size: Optional[Tuple[int, int]] = None, sample_base: int = 0):
+    """rt_render_frame_multi: row-interleaved bands on n_gpus devices + RCCL gather (one shot)."""
+    lib = load_library()
+    params, prims, cam = _frame_inputs(scene, camera_index, size)
     W, H = params.width, params.height
     s = np.zeros((W, H, 3), np.float64)
     n = np.zeros((W, H), np.uint32)
     m = np.zeros((W, H), np.uint32)
     rays = C.c_uint64(0)
-    prims = (rt_prim * max(1, scene.n_prims))(*scene.prims)
-    cam = rt_camera.from_buffer_copy(scene.cameras[camera_index])
     _check(lib.rt_render_frame_multi(C.byref(params), prims, scene.n_prims, C.byref(cam), n_gpus, spp, seed,
-                                     s.ctypes.data_as(C.POINTER(rt_color)), n.ctypes.data_as(C.POINTER(C.c_uint32)),
-                                     m.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(rays)))
+                                     sample_base, s.ctypes.data_as(C.POINTER(rt_color)),
+                                     n.ctypes.data_as(C.POINTER(C.c_uint32)), m.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                     C.byref(rays)))
     return s, n, m, rays.value
 
 

@@ -1155,15 +1155,17 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
     flush_counts<STATS>(wave_rays, cnt, p, lane);
 }
 
-__global__ void accumulate_kernel(PathParams p, double* sum, uint32_t* samples, uint32_t* misses)
+// plane: element stride between the R, G and B planes of sum (>= w*h; a gather slot may be taller
+// than the band set written into it)
+__global__ void accumulate_kernel(PathParams p, double* sum, uint32_t* samples, uint32_t* misses, size_t plane)
 {
     const int x = blockIdx.x * 16 + (threadIdx.x & 15);
     const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
     if (x >= p.w || y >= p.h) return;
     const size_t blk = (size_t)((y >> 3) * p.blocks_x + (x >> 3));
     const int q = (y & 7) * 8 + (x & 7);
-    const size_t npix = (size_t)p.w * p.h, i = (size_t)y * p.w + x;
-    double r = sum[i], g = sum[npix + i], bl = sum[2 * npix + i];
+    const size_t i = (size_t)y * p.w + x;
+    double r = sum[i], g = sum[plane + i], bl = sum[2 * plane + i];
     uint32_t ns = 0, nm = 0;
     const int used = (p.spp + p.chunk - 1) / p.chunk; // chunks past spp hold no partial
     for (int c = 0; c < used; c++) {
@@ -1176,8 +1178,8 @@ __global__ void accumulate_kernel(PathParams p, double* sum, uint32_t* samples, 
         nm += k >> 16;
     }
     sum[i] = r;
-    sum[npix + i] = g;
-    sum[2 * npix + i] = bl;
+    sum[plane + i] = g;
+    sum[2 * plane + i] = bl;
     samples[i] += ns;
     misses[i] += nm;
 }
@@ -1356,10 +1358,12 @@ hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams
                            stream);
 }
 
-hipError_t launch_accumulate(const PathParams& p, double* d_sum, uint32_t* d_samples, uint32_t* d_misses, hipStream_t stream)
+hipError_t launch_accumulate(const PathParams& p, double* d_sum, uint32_t* d_samples, uint32_t* d_misses, hipStream_t stream,
+                             size_t plane)
 {
+    if (plane == 0) plane = (size_t)p.w * p.h;
     dim3 grid((p.w + 15) / 16, (p.h + 15) / 16);
-    hipLaunchKernelGGL(accumulate_kernel, grid, dim3(256), 0, stream, p, d_sum, d_samples, d_misses);
+    hipLaunchKernelGGL(accumulate_kernel, grid, dim3(256), 0, stream, p, d_sum, d_samples, d_misses, plane);
     return hipGetLastError();
 }
 

@@ -51,9 +51,10 @@ hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams
                        int grid_blocks, hipStream_t stream, bool stats);
 int path_blocks_per_cu(int variant, size_t dyn_lds, bool stats);
 
-// partial -> fp64 planar accumulators (d_sum[3][w*h], d_samples, d_misses), added to.
+// partial -> fp64 planar accumulators (d_sum planes R | G | B, each `plane` doubles apart;
+// 0 = w*h), d_samples, d_misses (row-major w*h), added to.
 hipError_t launch_accumulate(const PathParams& p, double* d_sum, uint32_t* d_samples, uint32_t* d_misses,
-                             hipStream_t stream);
+                             hipStream_t stream, size_t plane = 0);
 // SampleSet.GetOutput over planar accumulators (row-major w*h) -> ARGB codes.
 hipError_t launch_tonemap(int w, int h, const double* d_sum, const uint32_t* d_samples, const uint32_t* d_misses,
                           rt_color back, double back_alpha, double exposure, int32_t* d_argb, hipStream_t stream);

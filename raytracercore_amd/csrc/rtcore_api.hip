@@ -151,20 +151,31 @@ struct rt_scene {
     CameraD camd{};
     CameraF camf{};
     DevBuf<CameraF> camf_d;     // the path kernels read the camera from device memory (not kernel arguments)
-    // ... and their launch parameters, from a ring of device slots filled from pinned host slots
-    // (a slot is reused kParamRing launches later, long after its launch has read it)
+    // ... and their launch parameters, from a ring of device slots filled from pinned host slots.
+    // A slot is rewritten kParamRing launches later; its event (recorded after the slot's upload)
+    // is waited on first, so a caller queueing more launches than that without a sync still
+    // hands every launch its own parameters.
     static constexpr int kParamRing = 256;
     DevBuf<PathParams> params_d;
     PathParams* params_h = nullptr;
+    std::array<hipEvent_t, kParamRing> slot_ev{};
     unsigned params_next = 0;
     bool has_camera = false;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // Launches share per-scene scratch (partials, work counter, stack overflow area).  The end of
+    // the last render operation is recorded here; an operation on a different stream waits for it.
+    hipEvent_t done_ev = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool any_op = false;
     uint64_t device_bytes = 0;
 
     ~rt_scene()
     {
         if (params_h) (void)hipHostFree(params_h);
+        for (hipEvent_t e : slot_ev)
+            if (e) (void)hipEventDestroy(e);
+        if (done_ev) (void)hipEventDestroy(done_ev);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         if (stream) (void)hipStreamDestroy(stream);
@@ -1050,6 +1061,7 @@ int resolve_traversal(rt_scene* s)
 
 PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint64_t seed, uint64_t base);
 int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t stream);
+int end_op(rt_scene* s, hipStream_t stream);
 
 // AUTO on a small scene: flat or grouped brute force?  Whether a group can be skipped depends on
 // how coherent a wave's rays are, which the camera decides, so each camera is calibrated once:
@@ -1081,6 +1093,7 @@ int calibrate_grouping(rt_scene* s)
     PathParams p = make_params(s, x0, y0, w, h, 2, 0x5EEDull, 0);
     p.pool = 64; // one chunk per pool: the counts must not depend on the pool size
     int rc = run_path(s, p, s->rays.p, s->stream);
+    if (rc == RT_OK) rc = end_op(s, s->stream);
     s->stats_on = was_on;
     s->stats_blocks_per_cu = was_blocks;
     s->variant = saved_variant;
@@ -1172,6 +1185,8 @@ int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t
     p.counter = s->counter.p;
     p.rays = d_rays;
     p.stats = s->stats_on ? s->stats_buf.p : nullptr;
+    // order after the previous operation when it ran on another stream (shared scratch)
+    if (s->any_op && stream != s->last_stream) HIP_TRY(hipStreamWaitEvent(stream, s->done_ev, 0));
     HIP_TRY(hipMemsetAsync(p.counter, 0, sizeof(unsigned int), stream));
     const int grid = s->n_cu * (s->stats_on ? s->stats_blocks_per_cu : s->blocks_per_cu);
     p.stack_ovf = nullptr;
@@ -1185,10 +1200,23 @@ int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t
         HIP_TRY(s->params_d.reserve(rt_scene::kParamRing));
     }
     const unsigned slot = s->params_next++ % rt_scene::kParamRing;
+    hipEvent_t& sev = s->slot_ev[slot];
+    if (sev) HIP_TRY(hipEventSynchronize(sev)); // the slot's previous upload has been read
+    else HIP_TRY(hipEventCreateWithFlags(&sev, hipEventDisableTiming));
     s->params_h[slot] = p;
     HIP_TRY(hipMemcpyAsync(s->params_d.p + slot, s->params_h + slot, sizeof(PathParams), hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipEventRecord(sev, stream));
     HIP_TRY(launch_path(s->dev, s->camf_d.p, s->params_d.p + slot, s->variant, grid, stream, s->stats_on));
     HIP_TRY(hipEventRecord(s->ev1, stream));
+    return RT_OK;
+}
+
+// Marks the end of a render operation (path kernel + the kernel that consumed its partials).
+int end_op(rt_scene* s, hipStream_t stream)
+{
+    HIP_TRY(hipEventRecord(s->done_ev, stream));
+    s->last_stream = stream;
+    s->any_op = true;
     return RT_OK;
 }
 
@@ -1536,6 +1564,7 @@ int rt_scene_create(const rt_scene_params* params, const rt_prim* prims, int32_t
     HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&s->ev0));
     HIP_TRY(hipEventCreate(&s->ev1));
+    HIP_TRY(hipEventCreateWithFlags(&s->done_ev, hipEventDisableTiming));
     using clk = std::chrono::steady_clock;
     auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
     const auto t0 = clk::now();
@@ -1643,7 +1672,7 @@ int rt_render_device(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, 
     rc = run_path(s, p, d_rays, st);
     if (rc != RT_OK) return rc;
     HIP_TRY(launch_accumulate(p, d_sum, d_samples, d_misses, st));
-    return RT_OK;
+    return end_op(s, st);
 }
 
 int rt_last_kernel_ms(rt_scene* s, float* ms)
@@ -1753,6 +1782,8 @@ int rt_render_tile_1spp(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t 
     rc = run_path(s, p, s->rays.p, s->stream);
     if (rc != RT_OK) return rc;
     HIP_TRY(launch_colors_1spp(p, s->colors.p, s->stream));
+    rc = end_op(s, s->stream);
+    if (rc != RT_OK) return rc;
     HIP_TRY(hipMemcpyAsync(out, s->colors.p, npix * sizeof(rt_color), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     return RT_OK;
@@ -1830,138 +1861,279 @@ int rt_bvh_counts(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, int
     return debug_pass_host(s, 1, x0, y0, w, h, counts_out, "rt_bvh_counts");
 }
 
-int rt_render_frame_multi(const rt_scene_params* params, const rt_prim* prims, int32_t n_prims,
-                          const rt_camera* camera, int32_t n_gpus, int32_t spp, uint64_t seed, rt_color* sum_rgb,
-                          uint32_t* samples, uint32_t* misses, uint64_t* rays_out)
+} // extern "C"
+
+// ------------------------------------------------------------------ row bands (multi-GPU) ----
+// A band set (band, stride, offset) is frame rows {y : (y / band) % stride == offset}: device g of
+// n owns set (16, n, g), interleaved for load balance (die.txt's background rows cost one ray per
+// sample).  On the device a set is rendered as a tile of band_set_rows() rows, tile row r being
+// frame row ((r / band) * stride + offset) * band + r % band (PathParams::band), into planar
+// accumulators whose planes are `plane` elements apart -- the slot of rt_frame's gather, sized for
+// the tallest set, so a shorter set leaves the end of each plane unused.
+struct rt_frame {
+    int n = 0, W = 0, H = 0, band = 16;
+    std::vector<int> rows;            // rows of device g's band set
+    size_t slot_pix = 0, slot_bytes = 0;
+    std::vector<rt_scene*> scenes;
+    std::vector<unsigned char*> sendb; // per device: one gather slot, Σr | Σg | Σb fp64, samples, misses u32
+    unsigned char* recvb = nullptr;    // device 0: n slots (n > 1)
+    unsigned char* host = nullptr;     // pinned copy of the gathered slots
+    std::vector<ncclComm_t> comms;
+    std::vector<unsigned long long> rays_h;
+
+    ~rt_frame()
+    {
+        for (ncclComm_t c : comms) (void)ncclCommDestroy(c);
+        for (int g = 0; g < (int)sendb.size(); g++)
+            if (sendb[g]) {
+                (void)hipSetDevice(scenes[g]->device);
+                (void)hipFree(sendb[g]);
+            }
+        if (recvb) {
+            (void)hipSetDevice(scenes[0]->device);
+            (void)hipFree(recvb);
+        }
+        if (host) (void)hipHostFree(host);
+        for (rt_scene* s : scenes)
+            if (s) rt_scene_destroy(s);
+    }
+};
+
+namespace {
+
+int band_set_rows(int H, int band, int stride, int offset)
 {
-    if (!params || !camera || !sum_rgb || !samples || !misses || spp <= 0 || n_gpus <= 0) {
+    int rows = 0;
+    for (int b = offset; b * band < H; b += stride) rows += std::min(band, H - b * band);
+    return rows;
+}
+
+// Largest band set of the split: the plane stride of a gather slot.
+int band_slot_rows(int H, int band, int stride)
+{
+    int m = 0;
+    for (int o = 0; o < stride; o++) m = std::max(m, band_set_rows(H, band, stride, o));
+    return m;
+}
+
+// Adds one band set's planar accumulators (device layout, planes `plane` apart) into frame buffers
+// in the C# [x, y] order (x * H + y).
+void scatter_band_set(const unsigned char* slot, size_t plane, int W, int H, int band, int stride, int offset,
+                      rt_color* sum_rgb, uint32_t* samples, uint32_t* misses)
+{
+    const double* hs = reinterpret_cast<const double*>(slot);
+    const uint32_t* hn = reinterpret_cast<const uint32_t*>(hs + 3 * plane);
+    const uint32_t* hm = hn + plane;
+    int tr = 0;
+    for (int b = offset; b * band < H; b += stride)
+        for (int y = b * band; y < std::min(H, (b + 1) * band); y++, tr++)
+            for (int x = 0; x < W; x++) {
+                const size_t i = (size_t)tr * W + x, o = (size_t)x * H + y;
+                sum_rgb[o].r += hs[i];
+                sum_rgb[o].g += hs[plane + i];
+                sum_rgb[o].b += hs[2 * plane + i];
+                samples[o] += hn[i];
+                misses[o] += hm[i];
+            }
+}
+
+// Queues one band set's render on stream: path kernel + accumulate into d_slot (added to).
+int render_band_set(rt_scene* s, int band, int stride, int offset, int rows, size_t plane, int spp, uint64_t seed,
+                    uint64_t sample_base, unsigned char* d_slot, unsigned long long* d_rays, hipStream_t stream)
+{
+    double* d_sum = reinterpret_cast<double*>(d_slot);
+    uint32_t* d_n = reinterpret_cast<uint32_t*>(d_sum + 3 * plane);
+    uint32_t* d_m = d_n + plane;
+    PathParams p = make_params(s, 0, 0, s->params.width, rows, spp, seed, sample_base);
+    p.band = band;
+    p.band_stride = stride;
+    p.band_offset = offset;
+    int rc = run_path(s, p, d_rays, stream);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(launch_accumulate(p, d_sum, d_n, d_m, stream, plane));
+    return end_op(s, stream);
+}
+
+} // namespace
+
+extern "C" {
+
+int rt_render_bands(rt_scene* s, int32_t band, int32_t band_stride, int32_t band_offset, int32_t spp, uint64_t seed,
+                    uint64_t sample_base, rt_color* sum_rgb, uint32_t* samples, uint32_t* misses, uint64_t* rays_out)
+{
+    if (!s || band <= 0 || band_stride <= 0 || band_offset < 0 || band_offset >= band_stride || spp < 0 || !sum_rgb ||
+        !samples || !misses) {
+        set_error("rt_render_bands: bad argument");
+        return RT_ERR_ARG;
+    }
+    if (!s->has_camera) {
+        set_error("no camera set (rt_scene_set_camera)");
+        return RT_ERR_STATE;
+    }
+    const int W = s->params.width, H = s->params.height;
+    const int rows = band_set_rows(H, band, band_stride, band_offset);
+    if (rows == 0 || spp == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    const size_t plane = (size_t)band_slot_rows(H, band, band_stride) * W; // rt_frame's slot layout
+    const size_t bytes = plane * (3 * sizeof(double) + 2 * sizeof(uint32_t));
+    DevBuf<unsigned char> slot;
+    HIP_TRY(slot.reserve(bytes));
+    HIP_TRY(hipMemsetAsync(slot.p, 0, bytes, s->stream));
+    HIP_TRY(hipMemsetAsync(s->rays.p, 0, sizeof(unsigned long long), s->stream));
+    int rc = render_band_set(s, band, band_stride, band_offset, rows, plane, spp, seed, sample_base, slot.p, s->rays.p,
+                             s->stream);
+    if (rc != RT_OK) return rc;
+    std::vector<unsigned char> host(bytes);
+    unsigned long long hr = 0;
+    HIP_TRY(hipMemcpyAsync(host.data(), slot.p, bytes, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipMemcpyAsync(&hr, s->rays.p, sizeof hr, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    scatter_band_set(host.data(), plane, W, H, band, band_stride, band_offset, sum_rgb, samples, misses);
+    if (rays_out) *rays_out += hr;
+    return RT_OK;
+}
+
+int rt_frame_create(const rt_scene_params* params, const rt_prim* prims, int32_t n_prims, const rt_camera* camera,
+                    int32_t n_gpus, rt_frame** out)
+{
+    if (!params || !camera || !out || n_gpus <= 0 || params->width <= 0 || params->height <= 0) {
+        set_error("rt_frame_create: bad argument");
+        return RT_ERR_ARG;
+    }
+    *out = nullptr;
+    if (n_gpus > rt_device_count()) {
+        set_error("rt_frame_create: not enough devices");
+        return RT_ERR_NODEVICE;
+    }
+    std::unique_ptr<rt_frame> f(new rt_frame);
+    f->n = n_gpus;
+    f->W = params->width;
+    f->H = params->height;
+    for (int g = 0; g < n_gpus; g++) f->rows.push_back(band_set_rows(f->H, f->band, n_gpus, g));
+    f->slot_pix = (size_t)band_slot_rows(f->H, f->band, n_gpus) * f->W;
+    f->slot_bytes = f->slot_pix * (3 * sizeof(double) + 2 * sizeof(uint32_t));
+    f->scenes.assign(n_gpus, nullptr);
+    f->sendb.assign(n_gpus, nullptr);
+    f->rays_h.assign(n_gpus, 0);
+    std::vector<int> devs(n_gpus);
+    for (int g = 0; g < n_gpus; g++) {
+        devs[g] = g;
+        int rc = rt_scene_create(params, prims, n_prims, g, &f->scenes[g]);
+        if (rc == RT_OK) rc = rt_scene_set_camera(f->scenes[g], camera);
+        if (rc != RT_OK) return rc;
+        HIP_TRY(hipSetDevice(g));
+        HIP_TRY(hipMalloc(&f->sendb[g], f->slot_bytes));
+    }
+    HIP_TRY(hipHostMalloc(&f->host, f->slot_bytes * n_gpus, hipHostMallocDefault));
+    if (n_gpus > 1) {
+        HIP_TRY(hipSetDevice(0));
+        HIP_TRY(hipMalloc(&f->recvb, f->slot_bytes * n_gpus));
+        f->comms.assign(n_gpus, nullptr);
+        if (ncclCommInitAll(f->comms.data(), n_gpus, devs.data()) != ncclSuccess) {
+            f->comms.clear();
+            set_error("rt_frame_create: ncclCommInitAll failed");
+            return RT_ERR_NCCL;
+        }
+    }
+    *out = f.release();
+    return RT_OK;
+}
+
+int rt_frame_set_camera(rt_frame* f, const rt_camera* camera)
+{
+    if (!f || !camera) {
+        set_error("rt_frame_set_camera: bad argument");
+        return RT_ERR_ARG;
+    }
+    for (rt_scene* s : f->scenes) {
+        int rc = rt_scene_set_camera(s, camera);
+        if (rc != RT_OK) return rc;
+    }
+    return RT_OK;
+}
+
+int rt_frame_render(rt_frame* f, int32_t spp, uint64_t seed, uint64_t sample_base, rt_color* sum_rgb,
+                    uint32_t* samples, uint32_t* misses, uint64_t* rays_out)
+{
+    if (!f || spp < 0 || !sum_rgb || !samples || !misses) {
+        set_error("rt_frame_render: bad argument");
+        return RT_ERR_ARG;
+    }
+    if (spp == 0) return RT_OK;
+    // every device renders its band set into its slot, concurrently (launches are asynchronous)
+    for (int g = 0; g < f->n; g++) {
+        rt_scene* s = f->scenes[g];
+        HIP_TRY(hipSetDevice(s->device));
+        HIP_TRY(hipMemsetAsync(f->sendb[g], 0, f->slot_bytes, s->stream));
+        HIP_TRY(hipMemsetAsync(s->rays.p, 0, sizeof(unsigned long long), s->stream));
+        if (f->rows[g] == 0) continue;
+        int rc = render_band_set(s, f->band, f->n, g, f->rows[g], f->slot_pix, spp, seed, sample_base, f->sendb[g],
+                                 s->rays.p, s->stream);
+        if (rc != RT_OK) return rc;
+    }
+    // the slots meet on device 0 through one RCCL gather over xGMI
+    const unsigned char* src = f->sendb[0];
+    if (f->n > 1) {
+        if (ncclGroupStart() != ncclSuccess) {
+            set_error("rt_frame_render: ncclGroupStart failed");
+            return RT_ERR_NCCL;
+        }
+        bool ok = true;
+        for (int g = 0; g < f->n; g++) {
+            HIP_TRY(hipSetDevice(f->scenes[g]->device));
+            ok &= ncclGather(f->sendb[g], g == 0 ? f->recvb : nullptr, f->slot_bytes, ncclUint8, 0, f->comms[g],
+                             f->scenes[g]->stream) == ncclSuccess;
+        }
+        ok &= ncclGroupEnd() == ncclSuccess;
+        if (!ok) {
+            set_error("rt_frame_render: ncclGather failed");
+            return RT_ERR_NCCL;
+        }
+        src = f->recvb;
+    }
+    for (int g = 0; g < f->n; g++) {
+        rt_scene* s = f->scenes[g];
+        HIP_TRY(hipSetDevice(s->device));
+        HIP_TRY(hipMemcpyAsync(&f->rays_h[g], s->rays.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
+    }
+    rt_scene* s0 = f->scenes[0];
+    HIP_TRY(hipSetDevice(s0->device));
+    HIP_TRY(hipMemcpyAsync(f->host, src, f->slot_bytes * f->n, hipMemcpyDeviceToHost, s0->stream));
+    for (int g = 0; g < f->n; g++) {
+        HIP_TRY(hipSetDevice(f->scenes[g]->device));
+        HIP_TRY(hipStreamSynchronize(f->scenes[g]->stream));
+    }
+    for (int g = 0; g < f->n; g++)
+        scatter_band_set(f->host + f->slot_bytes * g, f->slot_pix, f->W, f->H, f->band, f->n, g, sum_rgb, samples,
+                         misses);
+    if (rays_out)
+        for (auto r : f->rays_h) *rays_out += r;
+    return RT_OK;
+}
+
+void rt_frame_destroy(rt_frame* f)
+{
+    if (!f) return;
+    for (rt_scene* s : f->scenes)
+        if (s) {
+            (void)hipSetDevice(s->device);
+            (void)hipStreamSynchronize(s->stream);
+        }
+    delete f;
+}
+
+int rt_render_frame_multi(const rt_scene_params* params, const rt_prim* prims, int32_t n_prims,
+                          const rt_camera* camera, int32_t n_gpus, int32_t spp, uint64_t seed, uint64_t sample_base,
+                          rt_color* sum_rgb, uint32_t* samples, uint32_t* misses, uint64_t* rays_out)
+{
+    if (!sum_rgb || !samples || !misses || spp < 0) {
         set_error("rt_render_frame_multi: bad argument");
         return RT_ERR_ARG;
     }
-    int ndev = rt_device_count();
-    if (n_gpus > ndev) {
-        set_error("rt_render_frame_multi: not enough devices");
-        return RT_ERR_NODEVICE;
-    }
-    const int W = params->width, H = params->height, band = 16;
-    const int n_bands = (H + band - 1) / band;
-    // device g owns bands g, g + n, g + 2n, ... (row-interleaved for load balance)
-    std::vector<int> rows(n_gpus, 0);
-    for (int b = 0; b < n_bands; b++) rows[b % n_gpus] += std::min(band, H - b * band);
-    const int max_rows = *std::max_element(rows.begin(), rows.end());
-    const size_t slot_pix = (size_t)max_rows * W;
-    const size_t slot_bytes = slot_pix * (3 * sizeof(double) + 2 * sizeof(uint32_t));
-
-    std::vector<rt_scene*> scenes(n_gpus, nullptr);
-    std::vector<ncclComm_t> comms(n_gpus);
-    std::vector<int> devs(n_gpus);
-    std::vector<unsigned char*> sendb(n_gpus, nullptr);
-    unsigned char* recvb = nullptr;
-    int rc = RT_OK;
-    auto cleanup = [&]() {
-        for (int g = 0; g < n_gpus; g++) {
-            if (sendb[g]) {
-                (void)hipSetDevice(g);
-                (void)hipFree(sendb[g]);
-            }
-            if (scenes[g]) rt_scene_destroy(scenes[g]);
-        }
-        if (recvb) {
-            (void)hipSetDevice(0);
-            (void)hipFree(recvb);
-        }
-    };
-    for (int g = 0; g < n_gpus; g++) {
-        devs[g] = g;
-        rc = rt_scene_create(params, prims, n_prims, g, &scenes[g]);
-        if (rc == RT_OK) rc = rt_scene_set_camera(scenes[g], camera);
-        if (rc != RT_OK) {
-            cleanup();
-            return rc;
-        }
-        (void)hipSetDevice(g);
-        if (hipMalloc(&sendb[g], slot_bytes) != hipSuccess || hipMemset(sendb[g], 0, slot_bytes) != hipSuccess) {
-            set_error("rt_render_frame_multi: device allocation failed");
-            cleanup();
-            return RT_ERR_OOM;
-        }
-    }
-    (void)hipSetDevice(0);
-    if (hipMalloc(&recvb, slot_bytes * n_gpus) != hipSuccess) {
-        set_error("rt_render_frame_multi: device allocation failed");
-        cleanup();
-        return RT_ERR_OOM;
-    }
-    if (ncclCommInitAll(comms.data(), n_gpus, devs.data()) != ncclSuccess) {
-        set_error("rt_render_frame_multi: ncclCommInitAll failed");
-        cleanup();
-        return RT_ERR_NCCL;
-    }
-    std::vector<unsigned long long> hrays(n_gpus, 0);
-    for (int g = 0; g < n_gpus && rc == RT_OK; g++) {
-        rt_scene* s = scenes[g];
-        (void)hipSetDevice(g);
-        double* d_sum = reinterpret_cast<double*>(sendb[g]);
-        uint32_t* d_n = reinterpret_cast<uint32_t*>(d_sum + 3 * slot_pix);
-        uint32_t* d_m = d_n + slot_pix;
-        if (rows[g] == 0) continue;
-        (void)hipMemsetAsync(s->rays.p, 0, sizeof(unsigned long long), s->stream);
-        PathParams p = make_params(s, 0, 0, W, rows[g], spp, seed, 0);
-        p.band = band;
-        p.band_stride = n_gpus;
-        p.band_offset = g;
-        rc = run_path(s, p, s->rays.p, s->stream);
-        if (rc == RT_OK && launch_accumulate(p, d_sum, d_n, d_m, s->stream) != hipSuccess) rc = RT_ERR_HIP;
-    }
-    if (rc == RT_OK) {
-        ncclGroupStart();
-        for (int g = 0; g < n_gpus; g++) {
-            (void)hipSetDevice(g);
-            if (ncclGather(sendb[g], g == 0 ? recvb : nullptr, slot_bytes, ncclUint8, 0, comms[g], scenes[g]->stream) !=
-                ncclSuccess)
-                rc = RT_ERR_NCCL;
-        }
-        if (ncclGroupEnd() != ncclSuccess) rc = RT_ERR_NCCL;
-    }
-    std::vector<unsigned char> host;
-    if (rc == RT_OK) {
-        for (int g = 0; g < n_gpus; g++) {
-            (void)hipSetDevice(g);
-            (void)hipMemcpyAsync(&hrays[g], scenes[g]->rays.p, sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                                 scenes[g]->stream);
-            if (hipStreamSynchronize(scenes[g]->stream) != hipSuccess) rc = RT_ERR_HIP;
-        }
-        host.resize(slot_bytes * n_gpus);
-        (void)hipSetDevice(0);
-        if (hipMemcpy(host.data(), recvb, host.size(), hipMemcpyDeviceToHost) != hipSuccess) rc = RT_ERR_HIP;
-    }
-    for (int g = 0; g < n_gpus; g++) ncclCommDestroy(comms[g]);
-    if (rc == RT_OK) {
-        std::vector<int> seen(n_gpus, 0);
-        for (int b = 0; b < n_bands; b++) {
-            const int g = b % n_gpus;
-            const unsigned char* base = host.data() + slot_bytes * g;
-            const double* hs = reinterpret_cast<const double*>(base);
-            const uint32_t* hn = reinterpret_cast<const uint32_t*>(hs + 3 * slot_pix);
-            const uint32_t* hm = hn + slot_pix;
-            for (int r = 0; r < std::min(band, H - b * band); r++) {
-                const int tr = seen[g]++, y = b * band + r;
-                for (int x = 0; x < W; x++) {
-                    const size_t i = (size_t)tr * W + x, o = (size_t)x * H + y;
-                    sum_rgb[o].r += hs[i];
-                    sum_rgb[o].g += hs[slot_pix + i];
-                    sum_rgb[o].b += hs[2 * slot_pix + i];
-                    samples[o] += hn[i];
-                    misses[o] += hm[i];
-                }
-            }
-        }
-        if (rays_out)
-            for (auto r : hrays) *rays_out += r;
-    } else if (g_error.empty()) {
-        set_error("rt_render_frame_multi failed");
-    }
-    cleanup();
+    rt_frame* f = nullptr;
+    int rc = rt_frame_create(params, prims, n_prims, camera, n_gpus, &f);
+    if (rc == RT_OK) rc = rt_frame_render(f, spp, seed, sample_base, sum_rgb, samples, misses, rays_out);
+    rt_frame_destroy(f);
     return rc;
 }
 

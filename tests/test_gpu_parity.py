@@ -250,7 +250,69 @@ def test_frame_multi_single_device(rc, scenes):
     gpu = rc.GpuRaytracer(scene, 0, size=(96, 80))
     s2, n2, m2, r2 = gpu.render_tile(0, 0, 96, 80, 8, seed=4)
     assert np.array_equal(n, n2) and np.array_equal(m, m2) and r == r2
-    assert np.allclose(s, s2, rtol=1e-6, atol=1e-6)
+    assert np.array_equal(s, s2)
+
+
+@pytest.mark.parametrize("stride", [2, 3, 8])
+@pytest.mark.parametrize("size", [(100, 84), (64, 40), (40, 16)])
+def test_band_sets_compose_ragged(rc, scenes, stride, size):
+    """Every band set of a frame, rendered on one device through the rt_frame slot layout
+    (planes spaced for the tallest set) and scattered into one frame, equals a whole-frame
+    render bit for bit -- including splits whose sets differ in height (a short last band,
+    a set with fewer bands) and sets with no rows at all."""
+    scene = scenes["bounce.txt"]
+    W, H = size
+    gpu = rc.GpuRaytracer(scene, 0, size=size)
+    out = (np.zeros((W, H, 3)), np.zeros((W, H), np.uint32), np.zeros((W, H), np.uint32))
+    rays = 0
+    for off in range(stride):
+        rays += gpu.render_bands(16, stride, off, 6, seed=11, sample_base=5, out=out)[3]
+    s2, n2, m2, r2 = gpu.render_tile(0, 0, W, H, 6, seed=11, sample_base=5)
+    assert np.array_equal(out[1], n2) and np.array_equal(out[2], m2) and rays == r2
+    assert np.array_equal(out[0], s2)
+    assert np.all(n2 + m2 == 6)
+
+
+def test_frame_progressive_sample_base(rc, scenes):
+    """A persistent rt_frame called twice with disjoint sample ranges accumulates the same samples
+    as one call over both ranges (FullRaytracer's progressive refinement)."""
+    scene = scenes["die.txt"]
+    f = rc.GpuFrame(scene, 0, n_gpus=1, size=(72, 56))
+    out = f.render(8, seed=2, sample_base=0)
+    s, n, m, r = f.render(8, seed=2, sample_base=8, out=out[:3])
+    f.close()
+    gpu = rc.GpuRaytracer(scene, 0, size=(72, 56))
+    s2, n2, m2, r2 = gpu.render_tile(0, 0, 72, 56, 16, seed=2)
+    assert np.array_equal(n, n2) and np.array_equal(m, m2) and out[3] + r == r2
+    assert np.allclose(s, s2, rtol=1e-5, atol=1e-5)
+
+
+def test_many_launches_two_streams(rc, scenes):
+    """More launches than the launch-parameter ring holds (256), queued without a sync and
+    alternating between two streams into one set of device accumulators: every launch gets its
+    own parameters and the scene's shared scratch is never used by two launches at once."""
+    import torch
+
+    scene = scenes["bounce.txt"]
+    W, H, N = 32, 24, 300
+    gpu = rc.GpuRaytracer(scene, 0, size=(W, H))
+    dev = torch.device("cuda", 0)
+    d_sum = torch.zeros(3 * W * H, dtype=torch.float64, device=dev)
+    d_n = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    d_m = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    d_r = torch.zeros(1, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    for k in range(N):
+        gpu.render_device(0, 0, W, H, 1, 6, k, d_sum.data_ptr(), d_n.data_ptr(), d_m.data_ptr(), d_r.data_ptr(),
+                          streams[k % 2].cuda_stream)
+    torch.cuda.synchronize(dev)
+    s2, n2, m2, r2 = gpu.render_tile(0, 0, W, H, N, seed=6)
+    n = d_n.cpu().numpy().reshape(H, W).T
+    m = d_m.cpu().numpy().reshape(H, W).T
+    s = d_sum.cpu().numpy().reshape(3, H, W).transpose(2, 1, 0)
+    assert np.array_equal(n, n2) and np.array_equal(m, m2) and int(d_r.item()) == r2
+    assert np.allclose(s, s2, rtol=1e-5, atol=1e-5)
 
 
 def test_errors_fail_loudly(rc, scenes):

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol(rc):
     out = subprocess.run(["nm", "-D", "--defined-only", rc.LIB_PATH], capture_output=True, text=True).stdout
     exported = set(re.findall(r" T (rt_\w+)", out))
     assert set(names) <= exported
-    assert lib.rt_abi_version() == 1
+    assert lib.rt_abi_version() == rc.ABI_VERSION
 
 
 def test_library_has_gfx950_code_object(rc):
