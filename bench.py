@@ -8,9 +8,13 @@ the timed region.  One ray = one Scene.RayTrace call (Raytracer.cs:77); one samp
 GetColor(x, y) (misses included, FullRaytracer.cs:343).
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): weak
-scaling, each rank renders the same frame with its own disjoint sample range
-(sample_base = (step * N + rank) * spp), and the per-pixel accumulators are summed onto rank
-0 with one RCCL reduce per step (the progressive-refinement merge of FullRaytracer.cs:326-344).
+scaling.  A step is one frame of N * 256 samples per pixel; the frame's rows are dealt to the
+ranks as interleaved 8-row bands (rank r: bands r, r+N, ...), each rank renders its rows with
+all of the frame's samples (the same work as one GPU's step at N = 1), and the band
+accumulators are gathered onto rank 0 with one RCCL gather per step and added into the frame
+(the progressive merge of FullRaytracer.cs:326-344), overlapped with the next step's render.
+`--split samples` instead gives every rank the whole frame with a disjoint sample range and
+reduces the accumulators onto rank 0.
 """
 from __future__ import annotations
 
@@ -92,9 +96,14 @@ def roofline(cfg, fpr, bpr, rays, ms):
                     f"scene served on chip): {bpr * rays / secs / 1e9:.0f} GB/s"}
 
 
-def path_stats(gpu, W, H, spp, seed, d_bufs):
+def path_stats(gpu, W, H, spp, seed, d_rays):
     """One untimed instrumented launch: traversal work per ray segment and the wave-cycle split."""
-    d_sum, d_n, d_m, d_rays = d_bufs
+    import torch
+
+    dev = d_rays.device
+    d_sum = torch.zeros(3 * W * H, dtype=torch.float64, device=dev)
+    d_n = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    d_m = torch.zeros(W * H, dtype=torch.int32, device=dev)
     gpu.set_stats(True)
     d_rays.zero_()
     gpu.render_device(0, 0, W, H, spp, seed, 1 << 40, d_sum.data_ptr(), d_n.data_ptr(), d_m.data_ptr(),
@@ -147,6 +156,8 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--split", default="bands", choices=["bands", "samples"],
+                    help="multi-GPU split: interleaved row bands + gather (default) or sample ranges + reduce")
     args = ap.parse_args()
 
     import numpy as np
@@ -177,40 +188,75 @@ def main() -> int:
     gpu = rc.GpuRaytracer(scene, cam, device=local, size=(W, H), traversal=trav)
     info = gpu.info()
     npix = W * H
-    # frame accumulators (SampleSet[w, h]: sum RGB fp64, samples, misses) and two sets of one
-    # step's share: step k renders into set k % 2 while set (k-1) % 2 is reduced onto rank 0
+    # frame accumulators on rank 0 (SampleSet[w, h]: sum RGB fp64 planes, samples, misses)
     f_sum = torch.zeros(3 * npix, dtype=torch.float64, device=dev)
     f_n = torch.zeros(npix, dtype=torch.int32, device=dev)
     f_m = torch.zeros(npix, dtype=torch.int32, device=dev)
-    sets = [(torch.zeros_like(f_sum), torch.zeros_like(f_n), torch.zeros_like(f_m)) for _ in range(2)]
     d_rays = torch.zeros(1, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    from raytracercore_amd.sharding import merge_accumulators, sample_base
+    from raytracercore_amd import sharding
 
-    def step(k: int) -> None:
-        base = sample_base(k, rank, world, spp)
-        d_sum, d_n, d_m = sets[k % 2]
-        d_sum.zero_()
-        d_n.zero_()
-        d_m.zero_()
-        gpu.render_device(0, 0, W, H, spp, args.seed, base, d_sum.data_ptr(), d_n.data_ptr(), d_m.data_ptr(),
-                          d_rays.data_ptr(), stream)
+    if args.split == "bands":
+        # rank r renders the band set (BAND, N, r) of a frame of N * spp samples per pixel: the same
+        # per-GPU work at every N (weak scaling), one RCCL gather of the band slots per step
+        band = sharding.BAND
+        plane = sharding.slot_rows(H, world, band) * W
+        rows = sharding.row_index(H, world, band, device=dev)
+        frame_spp = spp * world
+        # two slot sets: step k renders into set k % 2 while set (k-1) % 2 is gathered and merged
+        slots = [torch.zeros(4 * plane, dtype=torch.float64, device=dev) for _ in range(2)]
+        glists = [[torch.empty_like(slots[0]) for _ in range(world)] if (rank == 0 and world > 1) else None
+                  for _ in range(2)]
 
-    def start_merge(k: int):
-        # one RCCL reduce per accumulator plane, asynchronous: the next step's render (enqueued
-        # after this call) overlaps it on the compute stream
-        return k, merge_accumulators(sets[k % 2], dist, async_op=True)
+        def step(k: int) -> None:
+            slot = slots[k % 2]
+            slot.zero_()
+            s_, n_, m_ = sharding.slot_views(slot, plane)
+            gpu.render_bands_device(band, world, rank, frame_spp, args.seed, k * frame_spp, s_.data_ptr(),
+                                    n_.data_ptr(), m_.data_ptr(), plane, d_rays.data_ptr(), stream)
 
-    def finish_merge(pending) -> None:
-        k, works = pending
-        for w in works:
-            w.wait()  # the compute stream waits for the reduce, not the host
-        if rank == 0:
+        def start_merge(k: int):
+            return k, sharding.gather_slots(slots[k % 2], glists[k % 2], dist, async_op=True)
+
+        def finish_merge(pending) -> None:
+            k, works = pending
+            for w in works:
+                w.wait()  # the compute stream waits for the gather, not the host
+            if rank == 0:
+                got = glists[k % 2] if world > 1 else [slots[k % 2]]
+                sharding.scatter_slots(f_sum, f_n, f_m, got, rows, W, plane)
+        expect_per_step = frame_spp
+        parallelism = (f"row bands x{world} (interleaved {band}-row bands, {frame_spp} spp per frame), "
+                       f"RCCL gather per step")
+    else:
+        # sample sharding: every rank renders the whole frame with its own sample range; one RCCL
+        # reduce per accumulator plane per step
+        sets = [(torch.zeros_like(f_sum), torch.zeros_like(f_n), torch.zeros_like(f_m)) for _ in range(2)]
+
+        def step(k: int) -> None:
+            base = sharding.sample_base(k, rank, world, spp)
             d_sum, d_n, d_m = sets[k % 2]
-            f_sum.add_(d_sum)
-            f_n.add_(d_n)
-            f_m.add_(d_m)
+            d_sum.zero_()
+            d_n.zero_()
+            d_m.zero_()
+            gpu.render_device(0, 0, W, H, spp, args.seed, base, d_sum.data_ptr(), d_n.data_ptr(), d_m.data_ptr(),
+                              d_rays.data_ptr(), stream)
+
+        def start_merge(k: int):
+            return k, sharding.merge_accumulators(sets[k % 2], dist, async_op=True)
+
+        def finish_merge(pending) -> None:
+            k, works = pending
+            for w in works:
+                w.wait()
+            if rank == 0:
+                d_sum, d_n, d_m = sets[k % 2]
+                f_sum.add_(d_sum)
+                f_n.add_(d_n)
+                f_m.add_(d_m)
+        expect_per_step = spp * world
+        parallelism = f"sample-sharded x{world}, RCCL reduce per step"
 
     def run(first: int, count: int) -> list:
         kernel_ms = []
@@ -249,12 +295,12 @@ def main() -> int:
     if rank == 0:
         n_all = f_n.cpu().numpy().astype(np.int64)
         m_all = f_m.cpu().numpy().astype(np.int64)
-        expect = spp * (args.steps + args.warmup) * world
+        expect = expect_per_step * (args.steps + args.warmup)
         if not np.all(n_all + m_all == expect):
             raise SystemExit(f"sample bookkeeping mismatch: {np.unique(n_all + m_all)} != {expect}")
-        my_rays_per_step = total_rays / (args.steps * world)
+        my_rays_per_step = total_rays / (args.steps * world)  # the average rank's launch
         avg_ms = sum(kernel_ms) / len(kernel_ms)
-        st = path_stats(gpu, W, H, max(1, spp // 16), args.seed, (*sets[0], d_rays))
+        st = path_stats(gpu, W, H, max(1, spp // 16), args.seed, d_rays)
         fpr = flops_per_ray(st, scene)
         bpr = bytes_per_ray(st, scene)
         out = {
@@ -272,7 +318,7 @@ def main() -> int:
             "data": "synthetic: the reference's own scene file (tests/golden/scenes) with seeded camera samples",
             "config": {"workload": f"{scene_file} camera {cam} {W}x{H} x {spp} spp per GPU per step",
                        "traversal": ["auto", "brute", "bvh4", "bvh2", "grouped"][info.traversal], "recursion": scene.params.recursion,
-                       "parallelism": f"sample-sharded x{world}, RCCL reduce per step"},
+                       "parallelism": parallelism},
             "samples_per_s": round(total_samples / elapsed, 1),
             "rays_per_sample": round(total_rays / total_samples, 4),
             "kernel_ms": round(avg_ms, 3),

@@ -266,7 +266,7 @@ int rt_scene_get_stats(rt_scene* scene, uint64_t* out, int32_t n);
 /*
  * Row bands.  A band set (band, stride, offset) is the frame rows y with
  * (y / band) % stride == offset.  rt_frame deals the rows of a frame to n devices as the sets
- * (16, n, g), g = 0..n-1: interleaved bands balance background-heavy rows, where the
+ * (8, n, g), g = 0..n-1: interleaved bands balance background-heavy rows, where the
  * reference's contiguous tiles (FullRaytracer.cs:71-72) would not.
  *
  * rt_render_bands renders one band set on one scene and adds it into whole-frame buffers
@@ -276,6 +276,20 @@ int rt_scene_get_stats(rt_scene* scene, uint64_t* out, int32_t n);
 int rt_render_bands(rt_scene* scene, int32_t band, int32_t band_stride, int32_t band_offset, int32_t spp,
                     uint64_t seed, uint64_t sample_base, rt_color* sum_rgb, uint32_t* samples,
                     uint32_t* misses, uint64_t* rays_out);
+
+/*
+ * Device-resident band-set render for hosts that run one process (or worker) per GPU: adds spp
+ * samples of every pixel of the set into planar accumulators, row-major over the set's rows in
+ * frame order: d_sum planes R | G | B each `plane` doubles apart, d_samples / d_misses `plane`
+ * elements each (plane = 0: rows of the tallest set of the split x width, the gather-slot layout
+ * of rt_frame).  Asynchronous on `stream`, like rt_render_device.
+ */
+int rt_render_bands_device(rt_scene* scene, int32_t band, int32_t band_stride, int32_t band_offset,
+                           int32_t spp, uint64_t seed, uint64_t sample_base, double* d_sum,
+                           uint32_t* d_samples, uint32_t* d_misses, uint64_t plane,
+                           unsigned long long* d_rays, void* stream);
+/* Rows of a frame of `height` rows in band set (band, band_stride, band_offset); host only. */
+int rt_band_rows(int32_t height, int32_t band, int32_t band_stride, int32_t band_offset);
 
 /*
  * Persistent whole-frame renderer over devices 0..n_gpus-1 of this process (replaces the

@@ -131,6 +131,9 @@ def load_library(path: str = "") -> C.CDLL:
                                             P(C.c_uint32), P(C.c_uint64)]),
         "rt_render_bands": (C.c_int, [C.c_void_p] + [C.c_int32] * 4 + [C.c_uint64, C.c_uint64, P(rt_color),
                                       P(C.c_uint32), P(C.c_uint32), P(C.c_uint64)]),
+        "rt_render_bands_device": (C.c_int, [C.c_void_p] + [C.c_int32] * 4 + [C.c_uint64, C.c_uint64] +
+                                   [C.c_void_p] * 3 + [C.c_uint64, C.c_void_p, C.c_void_p]),
+        "rt_band_rows": (C.c_int, [C.c_int32] * 4),
         "rt_frame_create": (C.c_int, [P(rt_scene_params), P(rt_prim), C.c_int32, P(rt_camera), C.c_int32,
                                       P(C.c_void_p)]),
         "rt_frame_set_camera": (C.c_int, [C.c_void_p, P(rt_camera)]),
@@ -337,6 +340,13 @@ class GpuRaytracer:
                                         m.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(rays)))
         return s, n, m, rays.value
 
+    def render_bands_device(self, band, band_stride, band_offset, spp, seed, sample_base, d_sum, d_samples, d_misses,
+                            plane, d_rays, stream: int = 0) -> None:
+        """rt_render_bands_device: asynchronous band-set render into device accumulators (pointers)."""
+        _check(self.lib.rt_render_bands_device(self.handle, band, band_stride, band_offset, spp, seed, sample_base,
+                                               C.c_void_p(d_sum), C.c_void_p(d_samples), C.c_void_p(d_misses), plane,
+                                               C.c_void_p(d_rays), C.c_void_p(stream)))
+
     def render_tile_1spp(self, x0: int, y0: int, w: int, h: int, seed: int = 0, sample_index: int = 0) -> np.ndarray:
         """Raytracer.Render one pass: DoubleColor[w, h] with Placeholder (-1) for misses."""
         out = np.empty((w, h, 3), np.float64)
@@ -426,6 +436,13 @@ class GpuFrame:
             self.close()
         except Exception:
             pass
+
+
+def band_rows_count(height: int, band: int, band_stride: int, band_offset: int) -> int:
+    """rt_band_rows: rows of band set (band, band_stride, band_offset) of a frame (host only)."""
+    n = load_library().rt_band_rows(height, band, band_stride, band_offset)
+    _check(min(n, 0))
+    return n
 
 
 def render_frame_multi(scene: ParsedScene, camera_index: int, n_gpus: int, spp: int, seed: int = 0,

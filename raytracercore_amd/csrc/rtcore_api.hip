@@ -1865,13 +1865,13 @@ int rt_bvh_counts(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, int
 
 // ------------------------------------------------------------------ row bands (multi-GPU) ----
 // A band set (band, stride, offset) is frame rows {y : (y / band) % stride == offset}: device g of
-// n owns set (16, n, g), interleaved for load balance (die.txt's background rows cost one ray per
+// n owns set (8, n, g), interleaved for load balance (die.txt's background rows cost one ray per
 // sample).  On the device a set is rendered as a tile of band_set_rows() rows, tile row r being
 // frame row ((r / band) * stride + offset) * band + r % band (PathParams::band), into planar
 // accumulators whose planes are `plane` elements apart -- the slot of rt_frame's gather, sized for
 // the tallest set, so a shorter set leaves the end of each plane unused.
 struct rt_frame {
-    int n = 0, W = 0, H = 0, band = 16;
+    int n = 0, W = 0, H = 0, band = 8; // 8-row bands: any split of 1080 or 2160 rows is within one band of even
     std::vector<int> rows;            // rows of device g's band set
     size_t slot_pix = 0, slot_bytes = 0;
     std::vector<rt_scene*> scenes;
@@ -1991,6 +1991,53 @@ int rt_render_bands(rt_scene* s, int32_t band, int32_t band_stride, int32_t band
     scatter_band_set(host.data(), plane, W, H, band, band_stride, band_offset, sum_rgb, samples, misses);
     if (rays_out) *rays_out += hr;
     return RT_OK;
+}
+
+int rt_render_bands_device(rt_scene* s, int32_t band, int32_t band_stride, int32_t band_offset, int32_t spp,
+                           uint64_t seed, uint64_t sample_base, double* d_sum, uint32_t* d_samples, uint32_t* d_misses,
+                           uint64_t plane, unsigned long long* d_rays, void* stream)
+{
+    if (!s || band <= 0 || band_stride <= 0 || band_offset < 0 || band_offset >= band_stride || spp <= 0 || !d_sum ||
+        !d_samples || !d_misses || !d_rays) {
+        set_error("rt_render_bands_device: bad argument");
+        return RT_ERR_ARG;
+    }
+    if (!s->has_camera) {
+        set_error("no camera set (rt_scene_set_camera)");
+        return RT_ERR_STATE;
+    }
+    const int W = s->params.width, H = s->params.height;
+    const int rows = band_set_rows(H, band, band_stride, band_offset);
+    if (plane == 0) plane = (uint64_t)band_slot_rows(H, band, band_stride) * W;
+    if (plane < (uint64_t)rows * W) {
+        set_error("rt_render_bands_device: plane stride smaller than the band set");
+        return RT_ERR_ARG;
+    }
+    if (rows == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    // the slot's sample/miss planes follow the sum planes only in rt_frame; here they are separate
+    // buffers, each row-major over the set with the same plane stride as the sums
+    double* sum = d_sum;
+    uint32_t* n = d_samples;
+    uint32_t* m = d_misses;
+    PathParams p = make_params(s, 0, 0, W, rows, spp, seed, sample_base);
+    p.band = band;
+    p.band_stride = band_stride;
+    p.band_offset = band_offset;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    int rc = run_path(s, p, d_rays, st);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(launch_accumulate(p, sum, n, m, st, (size_t)plane));
+    return end_op(s, st);
+}
+
+int rt_band_rows(int32_t height, int32_t band, int32_t band_stride, int32_t band_offset)
+{
+    if (height < 0 || band <= 0 || band_stride <= 0 || band_offset < 0 || band_offset >= band_stride) {
+        set_error("rt_band_rows: bad argument");
+        return RT_ERR_ARG;
+    }
+    return band_set_rows(height, band, band_stride, band_offset);
 }
 
 int rt_frame_create(const rt_scene_params* params, const rt_prim* prims, int32_t n_prims, const rt_camera* camera,

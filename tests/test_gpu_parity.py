@@ -273,6 +273,40 @@ def test_band_sets_compose_ragged(rc, scenes, stride, size):
     assert np.all(n2 + m2 == 6)
 
 
+@pytest.mark.parametrize("world", [1, 3])
+def test_band_sets_device_gather_layout(rc, scenes, world):
+    """bench.py's band split on the device: each band set rendered by rt_render_bands_device into a
+    gather slot and scattered into the frame (raytracercore_amd.sharding) equals a whole-frame
+    render bit for bit."""
+    import torch
+
+    from raytracercore_amd import sharding
+
+    scene = scenes["bounce.txt"]
+    W, H, spp = 100, 84, 6
+    gpu = rc.GpuRaytracer(scene, 0, size=(W, H))
+    dev = torch.device("cuda", 0)
+    plane = sharding.slot_rows(H, world) * W
+    d_r = torch.zeros(1, dtype=torch.int64, device=dev)
+    slots = []
+    for r in range(world):
+        slot = torch.zeros(4 * plane, dtype=torch.float64, device=dev)
+        s_, n_, m_ = sharding.slot_views(slot, plane)
+        gpu.render_bands_device(sharding.BAND, world, r, spp, 11, 5, s_.data_ptr(), n_.data_ptr(), m_.data_ptr(),
+                                plane, d_r.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+        slots.append(slot)
+    f_sum = torch.zeros(3 * W * H, dtype=torch.float64, device=dev)
+    f_n = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    f_m = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    sharding.scatter_slots(f_sum, f_n, f_m, slots, sharding.row_index(H, world, device=dev), W, plane)
+    torch.cuda.synchronize(dev)
+    s2, n2, m2, r2 = gpu.render_tile(0, 0, W, H, spp, seed=11, sample_base=5)
+    assert np.array_equal(f_n.cpu().numpy().reshape(H, W).T, n2)
+    assert np.array_equal(f_m.cpu().numpy().reshape(H, W).T, m2)
+    assert np.array_equal(f_sum.cpu().numpy().reshape(3, H, W).transpose(2, 1, 0), s2)
+    assert int(d_r.item()) == r2
+
+
 def test_frame_progressive_sample_base(rc, scenes):
     """A persistent rt_frame called twice with disjoint sample ranges accumulates the same samples
     as one call over both ranges (FullRaytracer's progressive refinement)."""

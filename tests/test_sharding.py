@@ -1,8 +1,10 @@
-"""World-size-2 gloo rehearsal of the multi-GPU split (CPU only).
+"""Gloo rehearsals (world size 2 and 3) of bench.py's multi-GPU splits (CPU only).
 
-Each rank renders its sample range with the CPU oracle (standing in for the GPU), the
-accumulators are reduced onto rank 0 exactly as bench.py does over RCCL, and the merged frame
-must equal one render of all sample ranges.  Also checks the row-band split covers the frame.
+The CPU oracle stands in for the GPU.  Row bands (the default): each rank renders its band set
+into a gather slot, the slots are gathered onto rank 0 and scattered into the frame exactly as
+bench.py does over RCCL, and the frame must equal one whole-frame render.  Sample sharding:
+each rank renders its sample range, the accumulators are reduced onto rank 0, and the merged
+frame must equal one render of all sample ranges.  Also checks the band split covers the frame.
 """
 import os
 import socket
@@ -13,6 +15,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from raytracercore_amd import sharding
 from raytracercore_amd.sharding import band_rows, merge_accumulators, sample_base
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -72,13 +75,108 @@ def test_sample_sharded_reduce_equals_single_render(tmp_path, async_merge):
     assert np.allclose(got["s"], s, rtol=1e-12, atol=1e-12)
 
 
-@pytest.mark.parametrize("h,world", [(1080, 8), (1080, 3), (37, 2), (16, 4)])
+BW, BH = 10, 27  # 4 bands of 8 rows and one of 3: ragged band sets at world 2 and 3
+
+
+def _band_slot(orc, rank, world, spp, seed):
+    """The rank's gather slot (sharding slot layout) rendered band by band by the oracle."""
+    plane = sharding.slot_rows(BH, world) * BW
+    slot = torch.zeros(4 * plane, dtype=torch.float64)
+    s_, n_, m_ = sharding.slot_views(slot, plane)
+    s3, n2, m2 = s_.view(3, -1, BW), n_.view(-1, BW), m_.view(-1, BW)
+    i = 0
+    for b in range(rank, (BH + sharding.BAND - 1) // sharding.BAND, world):
+        y0 = b * sharding.BAND
+        bh = min(sharding.BAND, BH - y0)
+        s, n, m, _ = orc.render_tile(0, y0, BW, bh, spp, seed=seed, sample_base=0)  # [x, y] order
+        s3[:, i:i + bh] = torch.from_numpy(s.transpose(2, 1, 0).copy())
+        n2[i:i + bh] = torch.from_numpy(n.T.astype(np.int32))
+        m2[i:i + bh] = torch.from_numpy(m.T.astype(np.int32))
+        i += bh
+    return slot, plane
+
+
+def _band_worker(rank, world, port, out_path):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    from oracle.oracle import OracleScene
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    orc = OracleScene.from_file(os.path.join(ROOT, "tests", "golden", "scenes", "bounce.txt"))
+    orc.set_size(BW, BH)
+    slot, plane = _band_slot(orc, rank, world, 4, 3)
+    glist = [torch.empty_like(slot) for _ in range(world)] if rank == 0 else None
+    for w in sharding.gather_slots(slot, glist, dist, async_op=True):
+        w.wait()
+    if rank == 0:
+        f_sum = torch.zeros(3 * BW * BH, dtype=torch.float64)
+        f_n = torch.zeros(BW * BH, dtype=torch.int32)
+        f_m = torch.zeros(BW * BH, dtype=torch.int32)
+        sharding.scatter_slots(f_sum, f_n, f_m, glist, sharding.row_index(BH, world), BW, plane)
+        np.savez(out_path, s=f_sum.numpy(), n=f_n.numpy(), m=f_m.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _whole_frame(spp, seed):
+    from oracle.oracle import OracleScene
+
+    orc = OracleScene.from_file(os.path.join(ROOT, "tests", "golden", "scenes", "bounce.txt"))
+    orc.set_size(BW, BH)
+    s, n, m, _ = orc.render_tile(0, 0, BW, BH, spp, seed=seed, sample_base=0)
+    return s.transpose(2, 1, 0).reshape(-1), n.T.reshape(-1), m.T.reshape(-1)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_band_gather_equals_whole_frame(tmp_path, world):
+    """bench.py's default merge: band-set slots gathered onto rank 0 and scattered into the frame
+    equal one whole-frame render bit for bit (ragged sets: 27 rows in bands of 8)."""
+    out = str(tmp_path / "bands.npz")
+    mp.spawn(_band_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    got = np.load(out)
+    s, n, m = _whole_frame(4, 3)
+    assert np.array_equal(got["n"], n) and np.array_equal(got["m"], m)
+    assert np.array_equal(got["s"], s)
+
+
+def test_band_scatter_single_rank():
+    """World size 1 (bench.py at N = 1): the rank's own slot is scattered without a collective."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    from oracle.oracle import OracleScene
+
+    orc = OracleScene.from_file(os.path.join(ROOT, "tests", "golden", "scenes", "bounce.txt"))
+    orc.set_size(BW, BH)
+    slot, plane = _band_slot(orc, 0, 1, 4, 3)
+    assert sharding.gather_slots(slot, [slot], None) == []
+    f_sum = torch.zeros(3 * BW * BH, dtype=torch.float64)
+    f_n = torch.zeros(BW * BH, dtype=torch.int32)
+    f_m = torch.zeros(BW * BH, dtype=torch.int32)
+    sharding.scatter_slots(f_sum, f_n, f_m, [slot], sharding.row_index(BH, 1), BW, plane)
+    s, n, m = _whole_frame(4, 3)
+    assert np.array_equal(f_n.numpy(), n) and np.array_equal(f_m.numpy(), m)
+    assert np.array_equal(f_sum.numpy(), s)
+
+
+@pytest.mark.parametrize("h,world", [(1080, 8), (1080, 3), (2160, 8), (37, 2), (16, 4)])
 def test_band_rows_partition_the_frame(h, world):
     owned = [band_rows(h, world, r) for r in range(world)]
     allrows = sorted(r for rows in owned for r in rows)
     assert allrows == list(range(h))
     sizes = [len(o) for o in owned]
-    assert max(sizes) - min(sizes) <= 16
+    assert max(sizes) - min(sizes) <= sharding.BAND
+    assert max(sizes) == sharding.slot_rows(h, world)
+
+
+@pytest.mark.parametrize("h,world", [(1080, 8), (1080, 3), (2160, 8), (37, 2), (16, 4), (27, 3)])
+def test_band_rows_match_library(rc, h, world):
+    """The Python split and the library's band sets (rt_band_rows, host only) agree."""
+    for r in range(world):
+        assert rc.band_rows_count(h, sharding.BAND, world, r) == len(band_rows(h, world, r))
 
 
 def test_sample_bases_disjoint():
