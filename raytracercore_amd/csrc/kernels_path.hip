@@ -474,7 +474,8 @@ __device__ __forceinline__ float acos_turn2(float u)
 struct Ray3 {
     V3 o, d;
 };
-__device__ __forceinline__ Ray3 camera_ray(const CameraF& c, float x, float y)
+template <class CamT> // CameraF, or CameraF in the constant address space (scalar loads)
+__device__ __forceinline__ Ray3 camera_ray(const CamT& c, float x, float y)
 {
     Ray3 r;
     if (c.kind == RT_CAMERA_FRUSTUM) {
@@ -491,7 +492,8 @@ __device__ __forceinline__ Ray3 camera_ray(const CameraF& c, float x, float y)
 }
 
 // Raytracer.GetCameraRay (Raytracer.cs:262-282)
-__device__ __forceinline__ void start_sample(const CameraF& cam, int x, int y, Sample& S)
+template <class CamT>
+__device__ __forceinline__ void start_sample(const CamT& cam, int x, int y, Sample& S)
 {
     const float sx = (float)x + next_u(S.rng);
     const float sy = (float)y + next_u(S.rng);
@@ -731,7 +733,8 @@ __device__ __forceinline__ void lane_init(Lane& L)
 // Lanes without a sample in flight close finished items and take new ones from the wave's
 // pool (one atomic per p.pool items: chunks of one 8x8 block), then start the next camera sample
 // of their item.
-__device__ __forceinline__ void refill(Lane& L, Sample& S, const PathParams& p, const PathScene& s, const CameraF& cam, int lane,
+template <class ParT, class CamT>
+__device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const PathScene& s, const CamT& cam, int lane,
                                       unsigned total)
 {
     const bool need = L.active && !L.live && (!L.item_open || L.cnt < 65536u);
@@ -819,8 +822,8 @@ __device__ __forceinline__ void bounce(Lane& L, Sample& S, const PathScene& s, c
     }
 }
 
-template <bool STATS>
-__device__ __forceinline__ void flush_counts(unsigned long long wave_rays, const Counters& cnt, const PathParams& p,
+template <bool STATS, class ParT>
+__device__ __forceinline__ void flush_counts(unsigned long long wave_rays, const Counters& cnt, const ParT& p,
                                              int lane)
 {
     // one 64-bit add per wave for the ray count (and the optional traversal counters)
@@ -846,6 +849,16 @@ __device__ __forceinline__ void flush_counts(unsigned long long wave_rays, const
         if (lane == 0) atomicMax(p.stats + 7, mx);
     }
 }
+
+// The camera and the launch parameters in the constant address space: uniform reads become
+// scalar loads (the kernels never write them).
+#ifdef __HIP_DEVICE_COMPILE__
+#define RT_AS_CONST __attribute__((address_space(4)))
+#else
+#define RT_AS_CONST // the host pass only needs the types
+#endif
+typedef RT_AS_CONST const CameraF CameraC;
+typedef RT_AS_CONST const PathParams ParamsC;
 
 // Brute-force megakernel: every loop iteration issues one closest-hit query per live lane
 // (the scene's records arrive through scalar loads) and shades it.
@@ -878,11 +891,13 @@ __global__ void __launch_bounds__(256, CULL ? RT_GROUPED_WAVES : RT_PATH_WAVES)
         {
             // the camera is read per iteration through scalar loads from an opaque pointer: that
             // keeps the compiler from holding ~28 camera words in SGPRs for the whole kernel
-            // (they spilled, with the kernel's other arguments, into VGPR lanes and scratch)
-            const CameraF* cp = camp;
+            // (they spilled, with the kernel's other arguments, into VGPR lanes and scratch).  The
+            // pointer is in the constant address space: through a generic pointer the compiler
+            // cannot rule out the kernel's own stores and emits per-lane flat loads instead.
+            const CameraC* cp = (const CameraC*)camp;
             asm volatile("" : "+s"(cp));
             // the launch parameters likewise (a device copy, see run_path)
-            const PathParams* pq = pp;
+            const ParamsC* pq = (const ParamsC*)pp;
             asm volatile("" : "+s"(pq));
             refill(L, S, *pq, s, *cp, lane, total);
         }
@@ -935,7 +950,7 @@ __global__ void __launch_bounds__(256, CULL ? RT_GROUPED_WAVES : RT_PATH_WAVES)
         }
     }
     if (exp_sink == 1234.5f) pp->partial[0].x = exp_sink;
-    flush_counts<STATS>(wave_rays, cnt, *pp, lane);
+    flush_counts<STATS>(wave_rays, cnt, *(const ParamsC*)pp, lane);
 }
 
 // BVH megakernel with decoupled traversal.  A loop iteration advances the traversing lanes by
