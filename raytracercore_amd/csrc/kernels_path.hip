@@ -768,8 +768,17 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
                     L.cnt = (unsigned)(min(p.spp, L.s_next + p.chunk) - L.s_next) << 16; // chunk <= 64
                     L.ar = L.ag = L.ab = 0.0f;
                     L.fx = p.x0 + px;
-                    L.fy = p.band > 0 ? p.y0 + ((py / p.band) * p.band_stride + p.band_offset) * p.band + py % p.band
-                                      : p.y0 + py;
+                    L.fy = p.y0 + py;
+                    if (p.band > 0) { // band set: tile row py -> frame row (wave-uniform branch)
+                        unsigned bq, br;
+                        if (p.band_log2 >= 0) {
+                            bq = (unsigned)py >> p.band_log2;
+                            br = (unsigned)py & (unsigned)(p.band - 1);
+                        } else {
+                            divmod((unsigned)py, (unsigned)p.band, p.inv_band, bq, br);
+                        }
+                        L.fy = p.y0 + ((int)bq * p.band_stride + p.band_offset) * p.band + (int)br;
+                    }
 #ifdef RT_EXP_CHEAP_PKEY // cost experiment: no pixel-key hashing
                     L.pkey = rt_key2{(unsigned)L.fx * 0x9E3779B9u, (unsigned)L.fy};
 #else

@@ -10,6 +10,8 @@ struct PathParams {
     int x0, y0, w, h;           // tile within the frame
     int band, band_stride, band_offset; // band > 0: tile row r is frame row
                                         // y0 + ((r / band) * band_stride + band_offset) * band + r % band
+    int band_log2;              // log2(band) for a power-of-two band, else -1 (divide by inv_band)
+    float inv_band;             // fp32 1 / band
     int spp;                    // samples per pixel in this launch
     int chunk;                  // samples per work item (a lane owns one item at a time)
     int n_chunks;               // ceil(spp / chunk) rounded up to a power of two (empty chunks are skipped)

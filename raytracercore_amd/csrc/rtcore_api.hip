@@ -1154,6 +1154,19 @@ PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint6
     return p;
 }
 
+// Band-set launch: tile row r is frame row ((r / band) * stride + offset) * band + r % band; the
+// kernel divides by a shift for power-of-two bands, else by the fp32 reciprocal.
+void set_band(PathParams& p, int band, int stride, int offset)
+{
+    p.band = band;
+    p.band_stride = stride;
+    p.band_offset = offset;
+    p.band_log2 = -1;
+    for (int k = 0; k < 31; k++)
+        if (band == (1 << k)) p.band_log2 = k;
+    p.inv_band = 1.0f / (float)band;
+}
+
 int check_tile(rt_scene* s, int x0, int y0, int w, int h)
 {
     if (!s) {
@@ -1945,9 +1958,7 @@ int render_band_set(rt_scene* s, int band, int stride, int offset, int rows, siz
     uint32_t* d_n = reinterpret_cast<uint32_t*>(d_sum + 3 * plane);
     uint32_t* d_m = d_n + plane;
     PathParams p = make_params(s, 0, 0, s->params.width, rows, spp, seed, sample_base);
-    p.band = band;
-    p.band_stride = stride;
-    p.band_offset = offset;
+    set_band(p, band, stride, offset);
     int rc = run_path(s, p, d_rays, stream);
     if (rc != RT_OK) return rc;
     HIP_TRY(launch_accumulate(p, d_sum, d_n, d_m, stream, plane));
@@ -2021,9 +2032,7 @@ int rt_render_bands_device(rt_scene* s, int32_t band, int32_t band_stride, int32
     uint32_t* n = d_samples;
     uint32_t* m = d_misses;
     PathParams p = make_params(s, 0, 0, W, rows, spp, seed, sample_base);
-    p.band = band;
-    p.band_stride = band_stride;
-    p.band_offset = band_offset;
+    set_band(p, band, band_stride, band_offset);
     hipStream_t st = static_cast<hipStream_t>(stream);
     int rc = run_path(s, p, d_rays, st);
     if (rc != RT_OK) return rc;
