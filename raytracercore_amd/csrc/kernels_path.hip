@@ -78,15 +78,15 @@ __device__ __forceinline__ void hit_tri(const TestRec& R, int slot, V3 o, V3 d, 
 
 // Sphere (Sphere.cs:50-155).  Primitive.RayTrace returns the first surviving root: the close
 // one (Inside = false) if it lies ahead and is not culled, otherwise the far one.
-__device__ __forceinline__ void hit_sph(const TestRec& R, int slot, V3 o, V3 d, int prev, const XformF* __restrict__ xf,
-                                        Best& b)
+template <class XfP> // const XformF*, generic or in the constant address space
+__device__ __forceinline__ void hit_sph(const TestRec& R, int slot, V3 o, V3 d, int prev, XfP xf, Best& b)
 {
     const int id = __float_as_int(R.meta.x);
     const uint32_t fl = __float_as_uint(R.meta.y);
     V3 oo = o, dd = d;
     float k = 1.0f; // object-space ray parameter -> world distance
     if (fl & F_TRANSFORMED) {
-        const XformF& X = xf[__float_as_int(R.r1.y)];
+        const XformF X = xf[__float_as_int(R.r1.y)];
         oo = xf_point(X.to_world, o);
         const V3 dl = xf_dir(X.to_world, d);
         k = __builtin_amdgcn_rsqf(dot(dl, dl)); // |to_obj * dd| = 1 / |to_world * d|
@@ -154,9 +154,8 @@ __device__ __forceinline__ void hit_rect(const RectRec& R, int sg, V3 o, V3 d, V
     b.sg = ok ? sg : b.sg;
 }
 
-template <int AXIS, bool SUB = false>
-__device__ __forceinline__ void rect_group(const RectRec* __restrict__ r, int n, V3 o, V3 d, V3 id, V3 oi, int prev,
-                                           Best& b)
+template <int AXIS, bool SUB = false, class RectP>
+__device__ __forceinline__ void rect_group(RectP r, int n, V3 o, V3 d, V3 id, V3 oi, int prev, Best& b)
 {
 #ifdef RT_EXP_RECT_UNROLL4
     for (; n >= 4; n -= 4, r += 4) {
@@ -173,9 +172,15 @@ __device__ __forceinline__ void rect_group(const RectRec* __restrict__ r, int n,
         hit_rect<AXIS, SUB>(r0, r0.sg, o, d, id, oi, prev, b);
         hit_rect<AXIS, SUB>(r1, r1.sg, o, d, id, oi, prev, b);
     }
-    if (n > 0) hit_rect<AXIS, SUB>(*r, r->sg, o, d, id, oi, prev, b);
+    if (n > 0) {
+        const RectRec r0 = r[0];
+        hit_rect<AXIS, SUB>(r0, r0.sg, o, d, id, oi, prev, b);
+    }
 #else
-    for (; n > 0; n--, r++) hit_rect<AXIS, SUB>(*r, r->sg, o, d, id, oi, prev, b);
+    for (; n > 0; n--, r++) {
+        const RectRec r0 = r[0];
+        hit_rect<AXIS, SUB>(r0, r0.sg, o, d, id, oi, prev, b);
+    }
 #endif
 }
 
@@ -243,11 +248,12 @@ __device__ __forceinline__ bool slab(float4 lo, float4 hi, V3 oi, V3 id, float t
 // Every primitive, group by group (GroupRec: x-rects | y-rects | z-rects | triangles | spheres).
 // The loop indices are wave-uniform, so the records arrive through scalar loads.  With CULL a
 // group is skipped when no lane of the wave meets its box before its current closest hit.
-template <bool CULL, bool STATS>
-__device__ __forceinline__ void trace_brute(const PathScene& s, const GroupRec* __restrict__ groups,
-                                            const TestRec* __restrict__ tests, const RectRec* __restrict__ rects,
-                                            const FrameRec* __restrict__ frames, const XformF* __restrict__ xf, V3 o,
-                                            V3 d, int prev, Best& b, unsigned& n_flat, unsigned& n_sph)
+// The record pointers are in the constant address space (RT_AS_CONST) or generic.
+// boxes: the frame array viewed as BoxRecs (they share it).
+template <bool CULL, bool STATS, class SceneT, class GroupP, class TestP, class RectP, class FrameP, class BoxP, class XfP>
+__device__ __forceinline__ void trace_brute(const SceneT& s, GroupP groups, TestP tests, RectP rects, FrameP frames,
+                                            BoxP boxes, XfP xf, V3 o, V3 d, int prev, Best& b, unsigned& n_flat,
+                                            unsigned& n_sph)
 {
     const V3 id = v3(slab_rcp(d.x), slab_rcp(d.y), slab_rcp(d.z));
     const V3 oi = o * id;
@@ -262,15 +268,16 @@ __device__ __forceinline__ void trace_brute(const PathScene& s, const GroupRec* 
             n_flat += G.n_rect[0] + G.n_rect[1] + G.n_rect[2] + G.n_flat_extra + (G.n_tri_sph & 0xFFFF);
             n_sph += G.n_tri_sph >> 16;
         }
-        const RectRec* r = rects + __float_as_int(G.lo.w);
+        RectP r = rects + __float_as_int(G.lo.w);
         rect_group<0>(r, G.n_rect[0], o, d, id, oi, prev, b);
         r += G.n_rect[0];
         rect_group<1>(r, G.n_rect[1], o, d, id, oi, prev, b);
         r += G.n_rect[1];
         rect_group<2>(r, G.n_rect[2], o, d, id, oi, prev, b);
-        const BoxRec* boxes = reinterpret_cast<const BoxRec*>(frames); // BoxRecs share the frame array
-        for (int j = G.frame_first + G.n_frames; j < G.frame_first + G.n_frames + G.n_boxes; j++)
-            hit_box<false>(boxes[j], o, d, id, oi, prev, b);
+        for (int j = G.frame_first + G.n_frames; j < G.frame_first + G.n_frames + G.n_boxes; j++) {
+            const BoxRec B = boxes[j];
+            hit_box<false>(B, o, d, id, oi, prev, b);
+        }
         // rectangles in a common affine frame: the ray mapped once, then the same rect tests (t is
         // invariant under the map; a local d of 0 gives an infinite or NaN t, which never hits)
 #ifndef RT_EXP_NO_FRAMES
@@ -279,13 +286,16 @@ __device__ __forceinline__ void trace_brute(const PathScene& s, const GroupRec* 
             const V3 lo = v3(dot4(F.r0, o), dot4(F.r1, o), dot4(F.r2, o));
             const V3 ld = v3(dot3(F.r0, d), dot3(F.r1, d), dot3(F.r2, d));
             const V3 lid = v3(rcp(ld.x), rcp(ld.y), rcp(ld.z));
-            const RectRec* fr = rects + F.rect_first;
+            RectP fr = rects + F.rect_first;
             rect_group<0, true>(fr, F.n_rect[0], lo, ld, lid, lo, prev, b);
             fr += F.n_rect[0];
             rect_group<1, true>(fr, F.n_rect[1], lo, ld, lid, lo, prev, b);
             fr += F.n_rect[1];
             rect_group<2, true>(fr, F.n_rect[2], lo, ld, lid, lo, prev, b);
-            if (F.box >= 0) hit_box<true>(boxes[F.box], lo, ld, lid, lo, prev, b);
+            if (F.box >= 0) {
+                const BoxRec B = boxes[F.box];
+                hit_box<true>(B, lo, ld, lid, lo, prev, b);
+            }
         }
 #endif
         int i = __float_as_int(G.hi.w);
@@ -310,8 +320,8 @@ __device__ __forceinline__ void trace_brute(const PathScene& s, const GroupRec* 
     }
 }
 
-__device__ __forceinline__ void hit_any(const TestRec& R, int slot, V3 o, V3 d, int prev, const XformF* __restrict__ xf,
-                                        Best& b)
+template <class XfP>
+__device__ __forceinline__ void hit_any(const TestRec& R, int slot, V3 o, V3 d, int prev, XfP xf, Best& b)
 {
     switch (__float_as_uint(R.meta.y) & KIND_MASK) {
     case RT_PRIM_TRIANGLE: hit_tri(R, slot, o, d, prev, b); break;
@@ -530,9 +540,9 @@ __device__ __forceinline__ float one_minus_exp2_2a(float a)
 
 // One bounce of Raytracer.GetColor after the closest-hit query.  Returns 0 to continue the
 // path, 1 if the sample ended with colour `col`, 2 if it ended as a miss (Placeholder).
-__device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict__ prims, const MatF* __restrict__ mats,
-                                     const XformF* __restrict__ xfs, const float4* __restrict__ vnormals,
-                                     const TestRec* __restrict__ tests, const Best& b,
+template <class SceneT, class VnP, class TestP>
+__device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ prims, const MatF* __restrict__ mats,
+                                     const XformF* __restrict__ xfs, VnP vnormals, TestP tests, const Best& b,
                                      Sample& S, V3& col)
 {
     if (b.sg < 0) {
@@ -570,8 +580,8 @@ __device__ __forceinline__ int shade(const PathScene& s, const PrimF* __restrict
         if (sph) { // ellipsoid: the world normal is an affine map of the world hit point
             n = normalize(xf_point(xfs[__float_as_int(P.b.z)].normal, pos));
         } else { // Triangle.GetNormal quirk: Normal is never set -> NaN when inside
-            const float4* vn = vnormals + 3 * id;
-            const TestRec& R = tests[b.sg >> 1]; // barycentrics (u, v) = rows 0, 1 of M (p, 1)
+            const VnP vn = vnormals + 3 * id;
+            const TestRec R = tests[b.sg >> 1]; // barycentrics (u, v) = rows 0, 1 of M (p, 1)
             const float u = dot4(R.r0, pos), v = dot4(R.r1, pos);
             n = normalize(madd(xyz(vn[2]), u + v, madd(xyz(vn[1]), v, xyz(vn[0]) * u)));
             if (gin) n = v3(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
@@ -682,8 +692,8 @@ struct ShadeRecs {
     const MatF* mats;
     const XformF* xfs;
 };
-template <bool LDS>
-__device__ __forceinline__ ShadeRecs stage_scene(const PathScene& s, const PrimF* prims_g, const MatF* mats_g,
+template <bool LDS, class SceneT>
+__device__ __forceinline__ ShadeRecs stage_scene(const SceneT& s, const PrimF* prims_g, const MatF* mats_g,
                                                  const XformF* xf, float4* lds_scene)
 {
     if (!LDS) return ShadeRecs{prims_g, mats_g, xf};
@@ -733,8 +743,8 @@ __device__ __forceinline__ void lane_init(Lane& L)
 // Lanes without a sample in flight close finished items and take new ones from the wave's
 // pool (one atomic per p.pool items: chunks of one 8x8 block), then start the next camera sample
 // of their item.
-template <class ParT, class CamT>
-__device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const PathScene& s, const CamT& cam, int lane,
+template <class ParT, class SceneT, class CamT>
+__device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const SceneT& s, const CamT& cam, int lane,
                                       unsigned total)
 {
     const bool need = L.active && !L.live && (!L.item_open || L.cnt < 65536u);
@@ -815,8 +825,9 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
 }
 
 // After a closest-hit query: one bounce of GetColor; a finished sample goes into the item's sums.
-__device__ __forceinline__ void bounce(Lane& L, Sample& S, const PathScene& s, const ShadeRecs& R, const float4* vnormals,
-                                       const TestRec* tests, const Best& b)
+template <class SceneT, class VnP, class TestP>
+__device__ __forceinline__ void bounce(Lane& L, Sample& S, const SceneT& s, const ShadeRecs& R, VnP vnormals, TestP tests,
+                                       const Best& b)
 {
     V3 col;
     const int r = shade(s, R.prims, R.mats, R.xfs, vnormals, tests, b, S, col);
@@ -880,11 +891,14 @@ __global__ void __launch_bounds__(256, CULL ? RT_GROUPED_WAVES : RT_PATH_WAVES)
                 const Node4Q* __restrict__ nodes4, const GroupRec* __restrict__ groups, const XformF* __restrict__ xf,
                 const MatF* __restrict__ mats_g, const float4* __restrict__ vnormals)
 {
+    // everything but the LDS staging is read from the launch record *pp (fill_launch) in the
+    // constant address space, by scalar loads where it is used (the by-value arguments are the
+    // BVH kernels'; held in SGPRs for the whole kernel they spilled into VGPR lanes here)
+    const ParamsC& P0 = *(const ParamsC*)pp;
     extern __shared__ float4 lds_scene[];
-    const ShadeRecs R = stage_scene<LDS>(s, prims_g, mats_g, xf, lds_scene);
+    const ShadeRecs R = stage_scene<LDS>(P0.scene, P0.prims, P0.mats, P0.xf, lds_scene);
     const int lane = threadIdx.x & 63;
-    const unsigned total = (unsigned)pp->n_chunks * (unsigned)pp->n_pad;
-    const int pln0 = s.n_bvh;
+    const unsigned total = (unsigned)P0.n_chunks * (unsigned)P0.n_pad;
     Lane L;
     lane_init(L);
     Sample S;
@@ -897,56 +911,66 @@ __global__ void __launch_bounds__(256, CULL ? RT_GROUPED_WAVES : RT_PATH_WAVES)
     while (true) {
         unsigned long long t0 = 0, t1 = 0, t2 = 0;
         if (STATS) t0 = __builtin_readcyclecounter();
-        {
-            // the camera is read per iteration through scalar loads from an opaque pointer: that
-            // keeps the compiler from holding ~28 camera words in SGPRs for the whole kernel
-            // (they spilled, with the kernel's other arguments, into VGPR lanes and scratch).  The
-            // pointer is in the constant address space: through a generic pointer the compiler
-            // cannot rule out the kernel's own stores and emits per-lane flat loads instead.
-            const CameraC* cp = (const CameraC*)camp;
-            asm volatile("" : "+s"(cp));
-            // the launch parameters likewise (a device copy, see run_path)
-            const ParamsC* pq = (const ParamsC*)pp;
-            asm volatile("" : "+s"(pq));
-            refill(L, S, *pq, s, *cp, lane, total);
-        }
+        // The camera and the launch record are read per iteration through scalar loads from an
+        // opaque pointer: that keeps the compiler from holding ~28 camera words and the scene
+        // fields in SGPRs for the whole kernel (they spilled into VGPR lanes and scratch).  The
+        // pointers are in the constant address space: through a generic pointer the compiler
+        // cannot rule out the kernel's own stores and emits per-lane flat loads instead.
+        const CameraC* cp = (const CameraC*)camp;
+        asm volatile("" : "+s"(cp));
+        const ParamsC* pq = (const ParamsC*)pp;
+        asm volatile("" : "+s"(pq));
+        const auto& sc = pq->scene;
+        refill(L, S, *pq, sc, *cp, lane, total);
         if (!__any(L.active)) break;
         if (STATS) t1 = __builtin_readcyclecounter();
 #ifdef RT_EXP_DUP_START // cost experiment: a second camera sample on a copy
         if (L.live) {
             Sample S2 = S;
             S2.rng.k0 ^= (unsigned)S.bounce;
-            start_sample(*camp, L.fx, L.fy, S2);
+            start_sample(*cp, L.fx, L.fy, S2);
             exp_sink += S2.o.x + S2.d.y;
         }
 #endif
         wave_rays += (unsigned)__popcll(__ballot(L.live)); // one Scene.RayTrace per live lane
         if (L.live) {
+            const auto tests = (const RT_AS_CONST TestRec*)pq->tests;
+            const auto rects = (const RT_AS_CONST RectRec*)pq->rects;
+            const auto frames = (const RT_AS_CONST FrameRec*)pq->frames;
+            const auto boxes = (const RT_AS_CONST BoxRec*)pq->frames;
+            const auto groups = (const RT_AS_CONST GroupRec*)pq->groups;
+            const auto xf = (const RT_AS_CONST XformF*)pq->xf;
+            const auto vnormals = (const RT_AS_CONST float4*)pq->vnormals;
             Best b{__builtin_huge_valf(), -1};
 #ifdef RT_EXP_DUP_TRACE // cost experiment: a second closest-hit query from a perturbed origin
             {
                 Best b2{__builtin_huge_valf(), -1};
                 unsigned u0 = 0, u1 = 0;
-            trace_brute<CULL, false>(s, groups, tests, rects, frames, xf, S.o + v3(exp_sink * 1e-30f, 0, 0), S.d,
-                                     S.prev, b2, u0, u1);
+                trace_brute<CULL, false>(sc, groups, tests, rects, frames, boxes, xf,
+                                         S.o + v3(exp_sink * 1e-30f, 0, 0), S.d, S.prev, b2, u0, u1);
                 exp_sink += b2.t;
             }
 #endif
 #ifndef RT_EXP_NO_TRACE // cost experiment: every camera ray misses (per-sample overhead alone)
-            trace_brute<CULL, STATS>(s, groups, tests, rects, frames, xf, S.o, S.d, S.prev, b, cnt.tris, cnt.sphs);
+            trace_brute<CULL, STATS>(sc, groups, tests, rects, frames, boxes, xf, S.o, S.d, S.prev, b, cnt.tris,
+                                     cnt.sphs);
 #endif
-            for (int i = pln0; i < pln0 + s.n_pln; i++) hit_plane(tests[i], i, S.o, S.d, S.prev, b);
+            const int pln0 = sc.n_bvh;
+            for (int i = pln0; i < pln0 + sc.n_pln; i++) {
+                const TestRec tr = tests[i];
+                hit_plane(tr, i, S.o, S.d, S.prev, b);
+            }
             if (STATS) t2 = __builtin_readcyclecounter();
 #ifdef RT_EXP_DUP_SHADE // cost experiment: a second bounce on a copy
             {
                 Sample S2 = S;
                 S2.rng.k0 ^= (unsigned)S.bounce;
                 V3 c2;
-                shade(s, R.prims, R.mats, R.xfs, vnormals, tests, b, S2, c2);
+                shade(sc, R.prims, R.mats, R.xfs, vnormals, tests, b, S2, c2);
                 exp_sink += c2.x + S2.d.x;
             }
 #endif
-            bounce(L, S, s, R, vnormals, tests, b);
+            bounce(L, S, sc, R, vnormals, tests, b);
         } else if (STATS) {
             t2 = __builtin_readcyclecounter();
         }
@@ -1345,8 +1369,7 @@ int path_blocks_per_cu(int variant, size_t dyn_lds, bool stats)
     return n;
 }
 
-hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams* d_params, int variant,
-                       int grid_blocks, hipStream_t stream, bool stats)
+void fill_launch(const DevScene& s, int variant, PathParams& p)
 {
     PathScene ps = make_path_scene(s);
     const int kernel = variant >> 1;
@@ -1364,18 +1387,35 @@ hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams
     ps.n_groups = grouped ? s.n_groups_gr : 1;
     ps.n_bvh = bvh ? s.pln0_bvh : grouped ? s.pln0_gr : s.pln0_bf;
     ps.n_slots = ps.n_bvh + s.n_pln;
+    p.scene = ps;
+    p.tests = bvh ? s.tests_bvh : grouped ? s.tests_gr : s.tests_bf;
+    p.rects = grouped ? s.rects_gr : s.rects_bf;
+    p.frames = grouped ? s.frames_gr : s.frames_bf;
+    p.prims = bvh ? s.prims_bvh : grouped ? s.prims_gr : s.prims_bf;
+    p.groups = grouped ? s.groups_gr : s.groups_bf;
+    p.xf = s.xf;
+    p.mats = s.mats;
+    p.vnormals = s.vnormals;
+}
+
+hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams* d_params, int variant,
+                       int grid_blocks, hipStream_t stream, bool stats)
+{
+    PathParams h{}; // the same launch record as the device copy: the BVH kernels take it as arguments
+    fill_launch(s, variant, h);
+    PathScene ps = h.scene;
     const CameraF* ca = d_cam;
     const PathParams* pa = d_params;
-    const TestRec* tests = bvh ? s.tests_bvh : grouped ? s.tests_gr : s.tests_bf;
-    const RectRec* rects = grouped ? s.rects_gr : s.rects_bf;
-    const FrameRec* frames = grouped ? s.frames_gr : s.frames_bf;
-    const PrimF* prims = bvh ? s.prims_bvh : grouped ? s.prims_gr : s.prims_bf;
+    const TestRec* tests = h.tests;
+    const RectRec* rects = h.rects;
+    const FrameRec* frames = h.frames;
+    const PrimF* prims = h.prims;
     const NodeF* nodes = s.nodes;
     const Node4Q* nodes4 = s.nodes4;
-    const GroupRec* groups = grouped ? s.groups_gr : s.groups_bf;
-    const XformF* xf = s.xf;
-    const MatF* mats = s.mats;
-    const float4* vn = s.vnormals;
+    const GroupRec* groups = h.groups;
+    const XformF* xf = h.xf;
+    const MatF* mats = h.mats;
+    const float4* vn = h.vnormals;
     void* args[] = {&ps, &ca, &pa, &tests, &rects, &frames, &prims, &nodes, &nodes4, &groups, &xf, &mats, &vn};
     const size_t dyn = path_dyn_lds(s, variant);
     return hipLaunchKernel(reinterpret_cast<const void*>(pick(variant, stats)), dim3(grid_blocks), dim3(256), args, dyn,

@@ -32,7 +32,22 @@ struct PathParams {
     int* stack_ovf;             // BVH kernels: traversal-stack overflow, RT_STACK_OVF entries per lane of the grid
     unsigned long long* stats;  // optional [7]: node visits, triangle tests, sphere tests (per lane);
                                 //   wave cycles in sample start, traversal, shading; wave iterations
+    // The scene as this launch's kernel variant walks it (fill_launch).  The brute-force kernels read
+    // these from the launch record by scalar loads where they are used, instead of holding them in
+    // SGPRs as kernel arguments for the whole kernel (which spilled into VGPR lanes).
+    PathScene scene;
+    const TestRec* tests;
+    const RectRec* rects;
+    const FrameRec* frames;
+    const PrimF* prims;
+    const GroupRec* groups;
+    const XformF* xf;
+    const MatF* mats;
+    const float4* vnormals;
 };
+
+// Sets p.scene and the record pointers of the given kernel variant's slot order.
+void fill_launch(const DevScene& s, int variant, PathParams& p);
 
 // mode 0: primary hit IDs, mode 1: reference-BVH node counts (DebugRaycaster BoundingVolumes)
 hipError_t launch_primary_ids(const DevScene& s, const CameraD& cam, int x0, int y0, int w, int h, int mode,

@@ -1212,6 +1212,7 @@ int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t
         HIP_TRY(hipHostMalloc(&s->params_h, sizeof(PathParams) * rt_scene::kParamRing, hipHostMallocDefault));
         HIP_TRY(s->params_d.reserve(rt_scene::kParamRing));
     }
+    fill_launch(s->dev, s->variant, p);
     const unsigned slot = s->params_next++ % rt_scene::kParamRing;
     hipEvent_t& sev = s->slot_ev[slot];
     if (sev) HIP_TRY(hipEventSynchronize(sev)); // the slot's previous upload has been read
