@@ -211,13 +211,14 @@ __device__ __forceinline__ void hit_box(const BoxRec& B, V3 o, V3 d, V3 id, V3 o
     int fe = 0, fo = 0;
     if (keep & 0x3Fu) { // some face keeps entry hits (wave-uniform)
         fe = te == nx ? sx : (te == ny ? 2 + sy : 4 + sz);
-        ok_e = meet & (__float_as_uint(te) < __float_as_uint(b.t)) & (((perm >> (4 * fe)) & 15u) != rel_prev);
-        if ((keep & 0x3Fu) != 0x3Fu) ok_e &= ((keep >> fe) & 1u) != 0;
+        // the keep bit is tested unconditionally: selecting on "every face keeps" cost more
+        ok_e = meet & (__float_as_uint(te) < __float_as_uint(b.t)) & (((perm >> (4 * fe)) & 15u) != rel_prev) &
+               (((keep >> fe) & 1u) != 0);
     }
     if (keep & 0x3F00u) { // some face keeps exit hits
         fo = tx == fx ? 1 - sx : (tx == fy ? 3 - sy : 5 - sz);
-        ok_x = meet & (__float_as_uint(tx) < __float_as_uint(b.t)) & (((perm >> (4 * fo)) & 15u) != rel_prev);
-        if ((keep & 0x3F00u) != 0x3F00u) ok_x &= ((keep >> (8 + fo)) & 1u) != 0;
+        ok_x = meet & (__float_as_uint(tx) < __float_as_uint(b.t)) & (((perm >> (4 * fo)) & 15u) != rel_prev) &
+               (((keep >> (8 + fo)) & 1u) != 0);
     }
     const bool ok = ok_e | ok_x;
     b.t = ok ? (ok_e ? te : tx) : b.t;
