@@ -300,6 +300,7 @@ def main() -> int:
             raise SystemExit(f"sample bookkeeping mismatch: {np.unique(n_all + m_all)} != {expect}")
         my_rays_per_step = total_rays / (args.steps * world)  # the average rank's launch
         avg_ms = sum(kernel_ms) / len(kernel_ms)
+        build = gpu.build_stats()  # of the timed launches (before the instrumented one below)
         st = path_stats(gpu, W, H, max(1, spp // 16), args.seed, d_rays)
         fpr = flops_per_ray(st, scene)
         bpr = bytes_per_ray(st, scene)
@@ -327,7 +328,7 @@ def main() -> int:
                            "lane_slots_per_ray": st["wave_iters_per_ray"],
                            "wave_cycles": st["cycles"]},
             "scene_build": {"builder": ["auto", "host", "gpu"][info.bvh_builder],
-                            **{k: round(v, 2) for k, v in gpu.build_stats().items()}},
+                            **{k: round(v, 2) for k, v in build.items()}},
         }
         traffic_file = os.path.join(ROOT, "profiles", "traffic", f"{args.config}.json")
         if os.path.exists(traffic_file) and args.spp == 0:  # PMC bytes of this launch shape (tools/profile.sh)

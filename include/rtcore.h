@@ -29,14 +29,17 @@
 #ifndef RTCORE_H
 #define RTCORE_H
 
+#ifndef __HIPCC_RTC__
 #include <stdint.h>
 #include <stddef.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define RTCORE_ABI_VERSION 2 /* 2: rt_frame_*, rt_render_bands, sample_base in rt_render_frame_multi */
+#define RTCORE_ABI_VERSION 3 /* 2: rt_frame_*, rt_render_bands, sample_base in rt_render_frame_multi;
+                                3: rt_set_jit, rt_scene_get_jit_error, build stats [15..17] */
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -163,8 +166,11 @@ typedef enum rt_bvh_builder {
    builder), [2] upload ms, [3] GPU builder device ms, [4] PLOC rounds, [5] wide nodes,
    [6] wide-tree stack need; flat brute-force layout: [7] single world rectangles,
    [8] world boxes, [9] frames, [10] frame boxes, [11] rectangles tested one by one in
-   frames, [12] other triangles, [13] spheres, [14] hot wide nodes staged in LDS */
-#define RT_BUILD_STATS_COUNT 15
+   frames, [12] other triangles, [13] spheres, [14] hot wide nodes staged in LDS;
+   scene-specialised kernel of the last brute-force launch (rt_set_jit): [15] status (1 in use,
+   0 not used, -1 build failed: see rt_scene_get_jit_error), [16] its hiprtc compile ms (0 when
+   it came from the cache), [17] 1 if it came from the in-process or on-disk cache */
+#define RT_BUILD_STATS_COUNT 18
 
 /* ---------------------------------------------------------------- library ---- */
 int rt_abi_version(void);
@@ -183,6 +189,20 @@ void rt_scene_destroy(rt_scene* scene);
 int rt_set_bvh_builder(int32_t builder);
 /* Copies min(n, RT_BUILD_STATS_COUNT) build statistics of the scene (see above). */
 int rt_scene_get_build_stats(const rt_scene* scene, double* out, int32_t n);
+/* Scene-specialised brute-force kernels (no reference counterpart: an MI355X code-generation
+   choice).  With on = 1 (the default; the environment variable RTCORE_JIT=0 makes the default
+   0) the brute-force traversals of scenes of <= 48 primitives launch a build of the path kernel
+   whose primitive records are compile-time constants, made with hiprtc on the first launch per
+   scene (and per camera for the grouped order) and cached in-process and on disk
+   (RTCORE_JIT_CACHE, else $HOME/.cache/rtcore_jit).  Same arithmetic and results as the generic
+   kernel, which runs when on = 0 or a build fails.  Process-wide; applies to later launches. */
+int rt_set_jit(int32_t on);
+/* The reason the last scene-specialised build of this scene failed ("" if none). */
+int rt_scene_get_jit_error(const rt_scene* scene, char* buf, int32_t cap);
+/* Host only (no device needed): compiles the embedded kernel sources for `arch` (e.g. "gfx950")
+   as a scene-specialised build of an empty scene; returns the code object size, or a negative
+   rt_status with the compiler log in `log` (may be NULL). */
+int rt_debug_jit_compile(const char* arch, int32_t grouped, char* log, int32_t cap);
 /* Validation: checks the device-resident BVH2 and wide tree against the primitives (every
    child box contains the primitives below it, each primitive in exactly one leaf, depth and
    stack within what the kernels were sized for).  RT_ERR_STATE with the finding otherwise. */

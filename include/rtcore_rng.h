@@ -28,7 +28,9 @@
 #ifndef RTCORE_RNG_H
 #define RTCORE_RNG_H
 
+#ifndef __HIPCC_RTC__
 #include <stdint.h>
+#endif
 
 #if defined(__HIPCC__)
 #define RT_HD __host__ __device__ inline __attribute__((always_inline))

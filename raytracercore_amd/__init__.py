@@ -23,7 +23,7 @@ LIB_PATH = os.path.join(_HERE, "librtcore_hip.so")
 REPO_ROOT = os.path.dirname(_HERE)
 
 RT_OK = 0
-ABI_VERSION = 2  # RTCORE_ABI_VERSION of include/rtcore.h
+ABI_VERSION = 3  # RTCORE_ABI_VERSION of include/rtcore.h
 RT_PRIM_TRIANGLE, RT_PRIM_SPHERE, RT_PRIM_PLANE = 0, 1, 2
 RT_FLAG_MIRROR, RT_FLAG_TWOSIDED, RT_FLAG_INVERT, RT_FLAG_HASNORMALS, RT_FLAG_TRANSFORMED = 1, 2, 4, 8, 16
 RT_CAMERA_FRUSTUM, RT_CAMERA_ORTHO = 0, 1
@@ -31,7 +31,22 @@ RT_TRAVERSAL_AUTO, RT_TRAVERSAL_BRUTE, RT_TRAVERSAL_BVH, RT_TRAVERSAL_BVH2, RT_T
 RT_BVH_BUILDER_AUTO, RT_BVH_BUILDER_HOST, RT_BVH_BUILDER_GPU = 0, 1, 2
 BUILD_STAT_NAMES = ("prepare_ms", "bvh_ms", "upload_ms", "gpu_build_ms", "ploc_rounds", "wide_nodes", "stack_need",
                     "flat_rects", "flat_boxes", "flat_frames", "flat_frame_boxes", "flat_frame_rects", "flat_tris",
-                    "flat_spheres", "hot_nodes")
+                    "flat_spheres", "hot_nodes", "jit_status", "jit_compile_ms", "jit_cached")
+
+
+def set_jit(on: bool) -> None:
+    """rt_set_jit: scene-specialised brute-force kernels (hiprtc) on or off, process-wide."""
+    _check(load_library().rt_set_jit(1 if on else 0))
+
+
+def jit_compile_check(arch: str = "gfx950", grouped: bool = False) -> int:
+    """rt_debug_jit_compile (host only): code-object bytes of a scene-specialised build of the
+    embedded kernel sources for `arch`; raises RtError with the compiler log on failure."""
+    buf = C.create_string_buffer(8192)
+    n = load_library().rt_debug_jit_compile(arch.encode(), 1 if grouped else 0, buf, len(buf))
+    if n < 0:
+        raise RtError(f"scene-specialised build failed: {buf.value.decode(errors='replace')}")
+    return n
 
 
 class RtError(RuntimeError):
@@ -115,6 +130,9 @@ def load_library(path: str = "") -> C.CDLL:
         "rt_set_bvh_builder": (C.c_int, [C.c_int32]),
         "rt_scene_get_build_stats": (C.c_int, [C.c_void_p, P(C.c_double), C.c_int32]),
         "rt_scene_check_bvh": (C.c_int, [C.c_void_p]),
+        "rt_set_jit": (C.c_int, [C.c_int32]),
+        "rt_scene_get_jit_error": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32]),
+        "rt_debug_jit_compile": (C.c_int, [C.c_char_p, C.c_int32, C.c_char_p, C.c_int32]),
         "rt_render_tile": (C.c_int, [C.c_void_p] + [C.c_int32] * 5 + [C.c_uint64, C.c_uint64,
                                      P(rt_color), P(C.c_uint32), P(C.c_uint32), P(C.c_uint64)]),
         "rt_render_tile_1spp": (C.c_int, [C.c_void_p] + [C.c_int32] * 4 + [C.c_uint64, C.c_uint64, P(rt_color)]),
@@ -291,6 +309,12 @@ class GpuRaytracer:
     def check_bvh(self) -> None:
         """rt_scene_check_bvh: structural validation of the device BVHs (raises RtError)."""
         _check(self.lib.rt_scene_check_bvh(self.handle))
+
+    def jit_error(self) -> str:
+        """rt_scene_get_jit_error: why the last scene-specialised build failed ("" if it did not)."""
+        buf = C.create_string_buffer(4096)
+        self.lib.rt_scene_get_jit_error(self.handle, buf, len(buf))
+        return buf.value.decode(errors="replace")
 
     def build_stats(self) -> dict:
         """rt_scene_get_build_stats: scene-creation timings and the BVH builder's figures."""

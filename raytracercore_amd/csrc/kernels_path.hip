@@ -793,7 +793,9 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
 #ifdef RT_EXP_CHEAP_PKEY // cost experiment: no pixel-key hashing
                     L.pkey = rt_key2{(unsigned)L.fx * 0x9E3779B9u, (unsigned)L.fy};
 #else
-                    L.pkey = rt_rng_pixel_key(p.seed_key, (unsigned long long)L.fy * (unsigned long long)s.width +
+                    // the frame width from the launch record (a scene-specialised build's constant
+                    // scene leaves it out, so one build serves every frame size)
+                    L.pkey = rt_rng_pixel_key(p.seed_key, (unsigned long long)L.fy * (unsigned long long)p.scene.width +
                                                               (unsigned long long)L.fx);
 #endif
                 }
@@ -878,19 +880,21 @@ __device__ __forceinline__ void flush_counts(unsigned long long wave_rays, const
 #else
 #define RT_AS_CONST // the host pass only needs the types
 #endif
+#ifdef RT_SCENE_CONST
+// rt_jit.cpp generates this header per scene (and camera, for the grouped order): the launch's
+// PathScene and its brute-force records as 32-bit words (kSceneW, kGroupsW, kRectsW, kFramesW,
+// kTestsW).  Every record field then folds into the instructions (literal operands cost what a
+// VGPR operand does on gfx950, an SGPR operand twice that), the primitive loops unroll and the
+// per-record flag branches resolve at compile time.
+#include "rt_scene_const.h"
+#endif
 typedef RT_AS_CONST const CameraF CameraC;
 typedef RT_AS_CONST const PathParams ParamsC;
 
 // Brute-force megakernel: every loop iteration issues one closest-hit query per live lane
 // (the scene's records arrive through scalar loads) and shades it.
 template <bool CULL, bool LDS, bool STATS>
-__global__ void __launch_bounds__(256, CULL ? RT_GROUPED_WAVES : RT_PATH_WAVES)
-    path_kernel(PathScene s, const CameraF* __restrict__ camp, const PathParams* __restrict__ pp,
-                const TestRec* __restrict__ tests,
-                const RectRec* __restrict__ rects, const FrameRec* __restrict__ frames,
-                const PrimF* __restrict__ prims_g, const NodeF* __restrict__ nodes,
-                const Node4Q* __restrict__ nodes4, const GroupRec* __restrict__ groups, const XformF* __restrict__ xf,
-                const MatF* __restrict__ mats_g, const float4* __restrict__ vnormals)
+__device__ __forceinline__ void path_body(const CameraF* __restrict__ camp, const PathParams* __restrict__ pp)
 {
     // everything but the LDS staging is read from the launch record *pp (fill_launch) in the
     // constant address space, by scalar loads where it is used (the by-value arguments are the
@@ -921,7 +925,11 @@ __global__ void __launch_bounds__(256, CULL ? RT_GROUPED_WAVES : RT_PATH_WAVES)
         asm volatile("" : "+s"(cp));
         const ParamsC* pq = (const ParamsC*)pp;
         asm volatile("" : "+s"(pq));
+#ifdef RT_SCENE_CONST
+        const PathScene& sc = *(const PathScene*)kSceneW;
+#else
         const auto& sc = pq->scene;
+#endif
         refill(L, S, *pq, sc, *cp, lane, total);
         if (!__any(L.active)) break;
         if (STATS) t1 = __builtin_readcyclecounter();
@@ -935,12 +943,21 @@ __global__ void __launch_bounds__(256, CULL ? RT_GROUPED_WAVES : RT_PATH_WAVES)
 #endif
         wave_rays += (unsigned)__popcll(__ballot(L.live)); // one Scene.RayTrace per live lane
         if (L.live) {
+#ifdef RT_SCENE_CONST // scene-specialised build (rt_jit.cpp): the records are compile-time constants
+            const auto tests = (const TestRec*)kTestsW;
+            const auto rects = (const RectRec*)kRectsW;
+            const auto frames = (const FrameRec*)kFramesW;
+            const auto boxes = (const BoxRec*)kFramesW;
+            const auto groups = (const GroupRec*)kGroupsW;
+            const auto xf = (const XformF*)kXfW;
+#else
             const auto tests = (const RT_AS_CONST TestRec*)pq->tests;
             const auto rects = (const RT_AS_CONST RectRec*)pq->rects;
             const auto frames = (const RT_AS_CONST FrameRec*)pq->frames;
             const auto boxes = (const RT_AS_CONST BoxRec*)pq->frames;
             const auto groups = (const RT_AS_CONST GroupRec*)pq->groups;
             const auto xf = (const RT_AS_CONST XformF*)pq->xf;
+#endif
             const auto vnormals = (const RT_AS_CONST float4*)pq->vnormals;
             Best b{__builtin_huge_valf(), -1};
 #ifdef RT_EXP_DUP_TRACE // cost experiment: a second closest-hit query from a perturbed origin
@@ -985,6 +1002,15 @@ __global__ void __launch_bounds__(256, CULL ? RT_GROUPED_WAVES : RT_PATH_WAVES)
     }
     if (exp_sink == 1234.5f) pp->partial[0].x = exp_sink;
     flush_counts<STATS>(wave_rays, cnt, *(const ParamsC*)pp, lane);
+}
+
+template <bool CULL, bool LDS, bool STATS>
+__global__ void __launch_bounds__(256, CULL ? RT_GROUPED_WAVES : RT_PATH_WAVES)
+    path_kernel(PathScene, const CameraF* __restrict__ camp, const PathParams* __restrict__ pp, const TestRec*,
+                const RectRec*, const FrameRec*, const PrimF*, const NodeF*, const Node4Q*, const GroupRec*,
+                const XformF*, const MatF*, const float4*)
+{
+    path_body<CULL, LDS, STATS>(camp, pp); // the other arguments are the BVH kernels' (same launch)
 }
 
 // BVH megakernel with decoupled traversal.  A loop iteration advances the traversing lanes by
@@ -1204,6 +1230,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
     flush_counts<STATS>(wave_rays, cnt, p, lane);
 }
 
+#ifndef __HIPCC_RTC__ // the host side and the other kernels (not part of a hiprtc build)
 // plane: element stride between the R, G and B planes of sum (>= w*h; a gather slot may be taller
 // than the band set written into it)
 __global__ void accumulate_kernel(PathParams p, double* sum, uint32_t* samples, uint32_t* misses, size_t plane)
@@ -1335,8 +1362,10 @@ PathScene make_path_scene(const DevScene& s)
     return ps;
 }
 
+#endif // __HIPCC_RTC__
 } // namespace
 
+#ifndef __HIPCC_RTC__
 int path_wide_stack() { return RT_WIDE_STACK; }
 
 size_t path_lds_bytes(const DevScene& s)
@@ -1448,4 +1477,15 @@ hipError_t launch_colors_1spp(const PathParams& p, double* d_out, hipStream_t st
     return hipGetLastError();
 }
 
+#endif // __HIPCC_RTC__
 } // namespace rtc
+
+#ifdef RT_SCENE_CONST
+// The entry point of a scene-specialised build (rt_jit.cpp): RT_SCENE_CONST_GROUPED selects the
+// grouped (culling) or the flat brute-force kernel; LDS staging of the shading records.
+extern "C" __global__ void __launch_bounds__(256, RT_SCENE_CONST_GROUPED ? RT_GROUPED_WAVES : RT_PATH_WAVES)
+    rt_path_const(const rtc::CameraF* __restrict__ camp, const rtc::PathParams* __restrict__ pp)
+{
+    rtc::path_body<RT_SCENE_CONST_GROUPED != 0, true, false>(camp, pp);
+}
+#endif

@@ -8,8 +8,10 @@
 //   * the FAST fp32 set (PrimF + NodeF): a binned-SAH BVH2 whose nodes carry both child
 //     boxes (one 64-B line per visit), used by the persistent path-tracing kernel.
 #pragma once
+#ifndef __HIPCC_RTC__ // hiprtc (the scene-specialised kernels, rt_jit.cpp) provides these itself
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 #include "../../include/rtcore.h"
 

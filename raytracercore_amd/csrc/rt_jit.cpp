@@ -1,0 +1,229 @@
+// rt_jit.cpp -- scene-specialised brute-force path kernels (see rt_jit.h), built with hiprtc.
+#include "rt_jit.h"
+
+#include <hip/hiprtc.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <filesystem>
+#include <fstream>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <unistd.h>
+
+#include "rt_jit_sources.h" // generated: kernels_path.hip and the headers it includes
+
+namespace rtc {
+
+namespace {
+
+std::atomic<int> g_jit{-1}; // -1: not yet read from RTCORE_JIT
+
+template <class T>
+void put_words(std::ostringstream& o, const char* name, const std::vector<T>& v)
+{
+    static_assert(sizeof(T) % 4 == 0, "records are whole words");
+    const size_t n = v.size() * sizeof(T) / 4;
+    std::vector<uint32_t> w(n ? n : 1, 0u);
+    if (n) std::memcpy(w.data(), v.data(), n * 4);
+    o << "__device__ static const uint32_t " << name << "[" << w.size() << "] __attribute__((aligned(16))) = {";
+    char buf[16];
+    for (size_t i = 0; i < w.size(); i++) {
+        std::snprintf(buf, sizeof buf, "%s0x%x", i ? "," : "", w[i]);
+        o << buf;
+    }
+    o << "};\n";
+}
+
+uint64_t fnv1a(uint64_t h, const void* p, size_t n)
+{
+    const unsigned char* c = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; i++) {
+        h ^= c[i];
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+std::string cache_dir()
+{
+    if (const char* e = std::getenv("RTCORE_JIT_CACHE")) return e;
+    if (const char* x = std::getenv("XDG_CACHE_HOME")) return std::string(x) + "/rtcore_jit";
+    if (const char* h = std::getenv("HOME")) return std::string(h) + "/.cache/rtcore_jit";
+    return "/tmp/rtcore_jit_" + std::to_string((unsigned)getuid());
+}
+
+bool read_file(const std::string& path, std::vector<char>& out)
+{
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    out.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+    return !out.empty();
+}
+
+void write_file_atomic(const std::string& dir, const std::string& path, const std::vector<char>& data)
+{
+    std::error_code ec;
+    std::filesystem::create_directories(dir, ec);
+    if (ec) return; // the cache is an optimisation only
+    const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
+    {
+        std::ofstream f(tmp, std::ios::binary);
+        if (!f) return;
+        f.write(data.data(), (std::streamsize)data.size());
+        if (!f) return;
+    }
+    std::filesystem::rename(tmp, path, ec);
+    if (ec) std::filesystem::remove(tmp, ec);
+}
+
+std::string main_source(bool grouped)
+{
+    return std::string("#include \"rt_jit_prelude.h\"\n#define RT_SCENE_CONST\n#define RT_SCENE_CONST_GROUPED ") +
+           (grouped ? "1" : "0") + "\n#include \"kernels_path.hip\"\n";
+}
+
+bool compile(const std::string& arch, const std::string& main_src, const std::string& header, std::vector<char>& code,
+             std::string& err)
+{
+    std::vector<const char*> names, texts;
+    for (int k = 0; k < kJitSrcCount; k++) {
+        names.push_back(kJitSrcNames[k]);
+        texts.push_back(kJitSrcTexts[k]);
+    }
+    names.push_back("rt_scene_const.h");
+    texts.push_back(header.c_str());
+    hiprtcProgram prog = nullptr;
+    if (hiprtcCreateProgram(&prog, main_src.c_str(), "rt_jit_main.hip", (int)names.size(), texts.data(), names.data()) !=
+        HIPRTC_SUCCESS) {
+        err = "hiprtcCreateProgram failed";
+        return false;
+    }
+    const std::string arch_opt = "--offload-arch=" + arch;
+    // the library's own kernel flags (Makefile HIPFLAGS): no fused multiply-adds the source does not
+    // write, no SLP packing (v_pk_* issue no faster than two plain ops on gfx950)
+    const char* opts[] = {arch_opt.c_str(), "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
+                          "-munsafe-fp-atomics"};
+    const hiprtcResult r = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof opts[0]), opts);
+    if (r != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        hiprtcGetProgramLogSize(prog, &n);
+        std::string log(n, '\0');
+        if (n) hiprtcGetProgramLog(prog, &log[0]);
+        err = "hiprtc: " + std::string(hiprtcGetErrorString(r)) + ": " + log.substr(0, 2000);
+        hiprtcDestroyProgram(&prog);
+        return false;
+    }
+    size_t n = 0;
+    hiprtcGetCodeSize(prog, &n);
+    code.resize(n);
+    hiprtcGetCode(prog, code.data());
+    hiprtcDestroyProgram(&prog);
+    return n > 0;
+}
+
+struct Entry {
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+};
+std::mutex g_mu;
+std::map<std::pair<int, uint64_t>, Entry> g_cache; // (device, key) -> loaded module (process lifetime)
+
+} // namespace
+
+bool jit_enabled()
+{
+    int v = g_jit.load();
+    if (v < 0) {
+        const char* e = std::getenv("RTCORE_JIT");
+        v = (e && e[0] == '0') ? 0 : 1;
+        int expect = -1;
+        g_jit.compare_exchange_strong(expect, v);
+        v = g_jit.load();
+    }
+    return v == 1;
+}
+
+void jit_set_enabled(bool on) { g_jit.store(on ? 1 : 0); }
+
+std::string jit_scene_header(const PathScene& ps, const std::vector<GroupRec>& groups,
+                             const std::vector<RectRec>& rects, const std::vector<FrameRec>& frames,
+                             const std::vector<TestRec>& tests, const std::vector<XformF>& xf)
+{
+    std::ostringstream o;
+    o << "// generated by rt_jit.cpp: one launch's scene as constants\n#pragma once\n";
+    PathScene p = ps;
+    p.hot4 = nullptr; // brute-force kernels only
+    p.n_hot4 = 0;
+    p.width = 0;      // read from the launch record (one build serves every frame size)
+    put_words(o, "kSceneW", std::vector<PathScene>{p});
+    put_words(o, "kGroupsW", groups);
+    put_words(o, "kRectsW", rects);
+    put_words(o, "kFramesW", frames);
+    put_words(o, "kTestsW", tests);
+    put_words(o, "kXfW", xf);
+    return o.str();
+}
+
+bool jit_kernel(int device, const std::string& header, bool grouped, JitKernel& out, std::string& err)
+{
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+        err = "hipGetDeviceProperties failed";
+        return false;
+    }
+    const std::string arch = prop.gcnArchName;
+    uint64_t key = 1469598103934665603ull;
+    key = fnv1a(key, "rtcore-jit-1", 12);
+    key = fnv1a(key, arch.data(), arch.size());
+    for (int k = 0; k < kJitSrcCount; k++) key = fnv1a(key, kJitSrcTexts[k], std::strlen(kJitSrcTexts[k]));
+    key = fnv1a(key, header.data(), header.size());
+    const std::string main_src = main_source(grouped);
+    key = fnv1a(key, main_src.data(), main_src.size());
+
+    std::lock_guard<std::mutex> lock(g_mu);
+    out = JitKernel{};
+    Entry& e = g_cache[{device, key}];
+    if (!e.mod) {
+        char hex[32];
+        std::snprintf(hex, sizeof hex, "%016llx", (unsigned long long)key);
+        const std::string dir = cache_dir(), path = dir + "/" + hex + ".co";
+        std::vector<char> code;
+        if (read_file(path, code)) {
+            out.from_cache = true;
+        } else {
+            const auto t0 = std::chrono::steady_clock::now();
+            if (!compile(arch, main_src, header, code, err)) {
+                g_cache.erase({device, key});
+                return false;
+            }
+            out.compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            write_file_atomic(dir, path, code);
+        }
+        if (hipModuleLoadData(&e.mod, code.data()) != hipSuccess ||
+            hipModuleGetFunction(&e.fn, e.mod, "rt_path_const") != hipSuccess) {
+            err = "loading the scene-specialised module failed";
+            if (e.mod) (void)hipModuleUnload(e.mod);
+            g_cache.erase({device, key});
+            return false;
+        }
+    } else {
+        out.from_cache = true;
+    }
+    out.fn = e.fn;
+    return true;
+}
+
+size_t jit_compile_check(const std::string& arch, bool grouped, std::string& err)
+{
+    const std::string header = jit_scene_header(PathScene{}, {}, {}, {}, {}, {});
+    std::vector<char> code;
+    if (!compile(arch, main_source(grouped), header, code, err)) return 0;
+    return code.size();
+}
+
+} // namespace rtc

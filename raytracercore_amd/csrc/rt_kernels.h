@@ -46,6 +46,7 @@ struct PathParams {
     const float4* vnormals;
 };
 
+#ifndef __HIPCC_RTC__ // host-side launch interface (not part of a hiprtc-compiled kernel)
 // Sets p.scene and the record pointers of the given kernel variant's slot order.
 void fill_launch(const DevScene& s, int variant, PathParams& p);
 
@@ -77,5 +78,7 @@ hipError_t launch_tonemap(int w, int h, const double* d_sum, const uint32_t* d_s
                           rt_color back, double back_alpha, double exposure, int32_t* d_argb, hipStream_t stream);
 // partial (1 spp) -> DoubleColor[w, h] in x*h + y order, Placeholder(-1) on a miss.
 hipError_t launch_colors_1spp(const PathParams& p, double* d_out, hipStream_t stream);
+
+#endif
 
 } // namespace rtc

@@ -10,6 +10,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -22,6 +23,7 @@
 #include "../../include/rtcore_rng.h"
 #include "bvh_gpu.h"
 #include "host_scene.h"
+#include "rt_jit.h"
 #include "rt_kernels.h"
 
 using namespace rtc;
@@ -127,6 +129,25 @@ struct rt_scene {
     DevBuf<FrameRec> frames_gr;
     DevBuf<GroupRec> groups_gr;
     std::vector<GroupRec> groups_gr_host; // in build order; uploaded nearest-first per camera
+    // host copies of the brute-force records (the scene-specialised kernels, rt_jit.h)
+    struct BruteHost {
+        std::vector<GroupRec> groups; // the grouped order: in the current camera's upload order
+        std::vector<RectRec> rects;
+        std::vector<FrameRec> frames;
+        std::vector<TestRec> tests;
+    } flat_h, grouped_h;
+    std::vector<XformF> xf_h;
+    unsigned group_order_gen = 0; // bumped when the grouped order's group order changes
+    struct {
+        int variant = -1;          // the variant and group order the function was built for
+        unsigned gen = 0;
+        hipFunction_t fn = nullptr;
+        int blocks_per_cu = 0;
+        int status = 0;            // 1 built, 0 not used (off, or a BVH / staged-less variant), -1 failed
+        double compile_ms = 0;
+        bool from_cache = false;
+        std::string error;
+    } jit;
     double grouped_measured = 0; // calibrated brute-force cost ratio flat / grouped (AUTO picks grouped above 1.25)
     DevBuf<NodeF> nodes;
     DevBuf<Node4Q> nodes4;
@@ -892,6 +913,9 @@ int upload_scene(rt_scene* s)
     HIP_TRY(s->frames_gr.upload(grouped.frames));
     HIP_TRY(s->groups_gr.upload(grouped.groups));
     s->groups_gr_host = grouped.groups;
+    s->flat_h = {flat.groups, flat.rects, flat.frames, flat.tests};
+    s->grouped_h = {grouped.groups, grouped.rects, grouped.frames, grouped.tests};
+    s->xf_h = xf;
     if (s->bvh.builder != RT_BVH_BUILDER_GPU) {
         HIP_TRY(s->prims_bvh.upload(bv));
         tbv.resize(tbv.size() + kTestSpares, TestRec{}); // spare records: the BVH leaf step loads past a leaf
@@ -1184,6 +1208,61 @@ int check_tile(rt_scene* s, int x0, int y0, int w, int h)
     return RT_OK;
 }
 
+// The scene-specialised kernel (rt_jit.h) of the current brute-force variant, built on first use
+// and again after a group-order change.  Returns 1 when it is to be launched, 0 to launch the
+// generic kernel: JIT off, the instrumented kernel, a BVH or unstaged variant, or a failed build
+// (the generic kernel computes the same; the failure is kept in s->jit.error).
+int prepare_jit(rt_scene* s)
+{
+    // The flat order only by default: unrolled in full, the grouped order's culled group loop ran
+    // slower (die.txt C3 36.6 -> 37.9 ms), presumably from the code size; RTCORE_JIT_GROUPED=1 builds it.
+    const char* eg = getenv("RTCORE_JIT_GROUPED");
+    const bool grouped_ok = eg && eg[0] == '1';
+    const bool eligible = jit_enabled() && !s->stats_on &&
+                          (s->variant == path_variant(0, true) || (grouped_ok && s->variant == path_variant(1, true)));
+    if (!eligible) {
+        s->jit.status = 0;
+        return 0;
+    }
+    const bool grouped = s->variant == path_variant(1, true);
+    const unsigned gen = grouped ? s->group_order_gen : 0;
+    if (s->jit.variant == s->variant && s->jit.gen == gen) return s->jit.fn ? 1 : 0;
+    s->jit.variant = s->variant;
+    s->jit.gen = gen;
+    s->jit.fn = nullptr;
+    PathParams lp{};
+    fill_launch(s->dev, s->variant, lp);
+    const auto& B = grouped ? s->grouped_h : s->flat_h;
+    const std::string header = jit_scene_header(lp.scene, B.groups, B.rects, B.frames, B.tests, s->xf_h);
+    if (const char* dump = getenv("RTCORE_JIT_DUMP")) { // inspection: the generated header of the last build
+        if (FILE* f = fopen(dump, "w")) {
+            fwrite(header.data(), 1, header.size(), f);
+            fclose(f);
+        }
+    }
+    JitKernel k;
+    std::string err;
+    if (!jit_kernel(s->device, header, grouped, k, err)) {
+        s->jit.status = -1;
+        s->jit.error = err;
+        return 0;
+    }
+    int n = 0;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, k.fn, 256, path_dyn_lds(s->dev, s->variant)) !=
+            hipSuccess ||
+        n < 1) {
+        s->jit.status = -1;
+        s->jit.error = "occupancy query of the scene-specialised kernel failed";
+        return 0;
+    }
+    s->jit.fn = k.fn;
+    s->jit.blocks_per_cu = n;
+    s->jit.status = 1;
+    s->jit.compile_ms = k.compile_ms;
+    s->jit.from_cache = k.from_cache;
+    return 1;
+}
+
 // Launch the path kernel for p (work buffers sized here), timing it with the scene's events.
 int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t stream)
 {
@@ -1207,6 +1286,8 @@ int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t
         HIP_TRY(s->stack_ovf.reserve((size_t)grid * 256 * kStackOverflow));
         p.stack_ovf = s->stack_ovf.p;
     }
+    const int jit = prepare_jit(s);
+    const int jit_grid = jit ? s->n_cu * s->jit.blocks_per_cu : 0;
     HIP_TRY(hipEventRecord(s->ev0, stream));
     if (!s->params_h) {
         HIP_TRY(hipHostMalloc(&s->params_h, sizeof(PathParams) * rt_scene::kParamRing, hipHostMallocDefault));
@@ -1220,7 +1301,15 @@ int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t
     s->params_h[slot] = p;
     HIP_TRY(hipMemcpyAsync(s->params_d.p + slot, s->params_h + slot, sizeof(PathParams), hipMemcpyHostToDevice, stream));
     HIP_TRY(hipEventRecord(sev, stream));
-    HIP_TRY(launch_path(s->dev, s->camf_d.p, s->params_d.p + slot, s->variant, grid, stream, s->stats_on));
+    if (jit) {
+        const CameraF* ca = s->camf_d.p;
+        const PathParams* pa = s->params_d.p + slot;
+        void* args[] = {&ca, &pa};
+        HIP_TRY(hipModuleLaunchKernel(s->jit.fn, jit_grid, 1, 1, 256, 1, 1,
+                                      (unsigned)path_dyn_lds(s->dev, s->variant), stream, args, nullptr));
+    } else {
+        HIP_TRY(launch_path(s->dev, s->camf_d.p, s->params_d.p + slot, s->variant, grid, stream, s->stats_on));
+    }
     HIP_TRY(hipEventRecord(s->ev1, stream));
     return RT_OK;
 }
@@ -1344,6 +1433,90 @@ int rt_debug_brute_layout(const rt_prim* prims, int32_t n_prims, int32_t* out, i
     return RT_OK;
 }
 
+// Experiment support: the flat brute-force order's records as 32-bit words (groups | rects |
+// frames | tests); counts = {groups, rects, frames, tests}.  Host code only.
+int rt_debug_flat_records(const rt_prim* prims, int32_t n_prims, uint32_t* out, int64_t cap_words, int32_t* counts)
+{
+    if (n_prims < 0 || (n_prims > 0 && !prims) || !out || !counts) {
+        set_error("rt_debug_flat_records: bad argument");
+        return RT_ERR_ARG;
+    }
+    const std::vector<HostPrim> H = prepare_prims(prims, n_prims);
+    const int n = (int)H.size();
+    std::vector<int> xf_index(n, -1);
+    int nb = 0, nx = 0;
+    for (int i = 0; i < n; i++) {
+        nb += H[i].kind != RT_PRIM_PLANE;
+        if (H[i].kind == RT_PRIM_SPHERE && (H[i].flags & F_TRANSFORMED)) xf_index[i] = nx++;
+    }
+    SahBvh sah;
+    if (nb > 0 && builder_for(nb) == RT_BVH_BUILDER_HOST) sah = build_sah_bvh(H, n > 256 ? 4 : 2);
+    const BruteOrders o = make_brute_orders(H, xf_index, sah);
+    const BruteOrder& f = o.flat;
+    size_t w = 0;
+    auto put = [&](const void* p, size_t bytes) {
+        const size_t k = bytes / 4;
+        if ((int64_t)(w + k) <= cap_words) memcpy(out + w, p, bytes);
+        w += k;
+    };
+    put(f.groups.data(), f.groups.size() * sizeof(GroupRec));
+    put(f.rects.data(), f.rects.size() * sizeof(RectRec));
+    put(f.frames.data(), f.frames.size() * sizeof(FrameRec));
+    put(f.tests.data(), f.tests.size() * sizeof(TestRec));
+    counts[0] = (int32_t)f.groups.size();
+    counts[1] = (int32_t)f.rects.size();
+    counts[2] = (int32_t)f.frames.size();
+    counts[3] = (int32_t)f.tests.size();
+    if ((int64_t)w > cap_words) {
+        set_error("rt_debug_flat_records: buffer too small");
+        return RT_ERR_ARG;
+    }
+    return RT_OK;
+}
+
+int rt_set_jit(int32_t on)
+{
+    if (on != 0 && on != 1) {
+        set_error("rt_set_jit: on must be 0 or 1");
+        return RT_ERR_ARG;
+    }
+    jit_set_enabled(on == 1);
+    return RT_OK;
+}
+
+int rt_debug_jit_compile(const char* arch, int32_t grouped, char* log, int32_t cap)
+{
+    if (!arch || (grouped != 0 && grouped != 1)) {
+        set_error("rt_debug_jit_compile: bad argument");
+        return RT_ERR_ARG;
+    }
+    std::string err;
+    const size_t n = jit_compile_check(arch, grouped == 1, err);
+    if (log && cap > 0) {
+        const size_t k = std::min((size_t)cap - 1, err.size());
+        memcpy(log, err.data(), k);
+        log[k] = '\0';
+    }
+    if (n == 0) {
+        set_error("rt_debug_jit_compile: " + err);
+        return RT_ERR_STATE;
+    }
+    return (int)std::min(n, (size_t)0x7fffffff);
+}
+
+int rt_scene_get_jit_error(const rt_scene* s, char* buf, int32_t cap)
+{
+    if (!s || !buf || cap <= 0) {
+        set_error("rt_scene_get_jit_error: bad argument");
+        return RT_ERR_ARG;
+    }
+    const std::string& e = s->jit.error;
+    const size_t n = std::min((size_t)cap - 1, e.size());
+    memcpy(buf, e.data(), n);
+    buf[n] = '\0';
+    return (int)e.size();
+}
+
 int rt_scene_get_build_stats(const rt_scene* s, double* out, int32_t n)
 {
     if (!s || !out || n < 0) {
@@ -1355,7 +1528,8 @@ int rt_scene_get_build_stats(const rt_scene* s, double* out, int32_t n)
                                            (double)s->bvh.rounds, (double)s->bvh.n_nodes4, (double)s->bvh.stack4,
                                            (double)L.rects, (double)L.boxes, (double)L.frames, (double)L.frame_boxes,
                                            (double)L.frame_rects, (double)L.tris, (double)L.sphs,
-                                           (double)s->dev.n_hot4};
+                                           (double)s->dev.n_hot4, (double)s->jit.status, s->jit.compile_ms,
+                                           s->jit.from_cache ? 1.0 : 0.0};
     for (int i = 0; i < n && i < RT_BUILD_STATS_COUNT; i++) out[i] = v[i];
     return RT_OK;
 }
@@ -1626,6 +1800,10 @@ int rt_scene_set_camera(rt_scene* s, const rt_camera* cam)
         };
         std::stable_sort(g.begin(), g.end(), [&](const GroupRec& a, const GroupRec& b) { return dist2(a) < dist2(b); });
         HIP_TRY(hipMemcpy(s->groups_gr.p, g.data(), g.size() * sizeof(GroupRec), hipMemcpyHostToDevice));
+        if (memcmp(g.data(), s->grouped_h.groups.data(), g.size() * sizeof(GroupRec)) != 0) {
+            s->grouped_h.groups = g;
+            s->group_order_gen++;
+        }
     }
     s->has_camera = true;
     return calibrate_grouping(s);

@@ -10,6 +10,7 @@
   Recursion + 1.
 """
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -597,3 +598,57 @@ def test_random_box_scenes_agree(rc, seed):
     assert float(np.mean(np.sum((mean_a - mean_b) ** 2, axis=-1)[both])) < 1e-4
     orc = _oracle(rc, scene, (40, 30))
     assert (a.primary_ids() == orc.primary_ids()).all()
+
+
+@pytest.mark.parametrize("name,mode", [("bounce.txt", "BRUTE"), ("die.txt", "GROUPED"), ("die.txt", "BRUTE"),
+                                       ("BOXES3", "BRUTE"), ("BOXES5", "GROUPED")])
+def test_scene_specialised_kernel_matches_generic(rc, scenes, name, mode):
+    """The hiprtc build with the scene's records as constants (rt_set_jit) computes exactly what the
+    generic brute-force kernel computes: bit-identical sums, counts and ray totals."""
+    if name.startswith("BOXES"):
+        scene = rc.SceneLoader.from_text(_random_box_scene(int(name[5:])))
+    else:
+        scene = scenes[name]
+    trav = getattr(rc, "RT_TRAVERSAL_" + mode)
+    out = {}
+    os.environ["RTCORE_JIT_GROUPED"] = "1"  # the grouped order's build is opt-in (slower on die.txt)
+    try:
+        for on in (True, False):
+            rc.set_jit(on)
+            g = rc.GpuRaytracer(scene, 0, size=(96, 64), traversal=trav)
+            out[on] = g.render_tile(8, 4, 80, 56, 24, seed=11, sample_base=5)
+            st = g.build_stats()
+            assert st["jit_status"] == (1.0 if on else 0.0), g.jit_error()
+            g.close()
+    finally:
+        rc.set_jit(True)
+        del os.environ["RTCORE_JIT_GROUPED"]
+    (sa, na, ma, ra), (sb, nb, mb, rb) = out[True], out[False]
+    assert ra == rb and np.array_equal(na, nb) and np.array_equal(ma, mb)
+    assert np.array_equal(sa, sb)
+
+
+def test_scene_specialised_kernel_follows_camera_group_order(rc, scenes):
+    """Grouped order: the groups are re-sorted per camera, and the specialised build follows."""
+    os.environ["RTCORE_JIT_GROUPED"] = "1"
+    try:
+        _grouped_camera_switch(rc, scenes)
+    finally:
+        del os.environ["RTCORE_JIT_GROUPED"]
+
+
+def _grouped_camera_switch(rc, scenes):
+    g = rc.GpuRaytracer(scenes["die.txt"], 0, size=(64, 48), traversal=rc.RT_TRAVERSAL_GROUPED)
+    a0 = g.render_tile(0, 0, 64, 48, 8, seed=3)
+    cam2 = rc.rt_camera.from_buffer_copy(scenes["die.txt"].cameras[2])
+    C_ = __import__("ctypes")
+    assert g.lib.rt_scene_set_camera(g.handle, C_.byref(cam2)) == 0
+    a2 = g.render_tile(0, 0, 64, 48, 8, seed=3)
+    assert g.build_stats()["jit_status"] == 1.0
+    rc.set_jit(False)
+    try:
+        b2 = g.render_tile(0, 0, 64, 48, 8, seed=3)
+    finally:
+        rc.set_jit(True)
+    assert a2[3] == b2[3] and np.array_equal(a2[0], b2[0]) and np.array_equal(a2[1], b2[1])
+    assert not np.array_equal(a0[0], a2[0])

@@ -234,3 +234,10 @@ HEAD = "size 16 12\ncamera 0 -6 1, 0 0 0, 0 0 1, 60\n"
 def test_brute_layout_detection(rc, text, expect):
     got = _layout(rc, HEAD + text)
     assert {k: got[k] for k in expect} == expect
+
+
+@pytest.mark.parametrize("grouped", [False, True])
+def test_scene_specialised_build_compiles(rc, grouped):
+    """The kernel sources embedded in the library compile with hiprtc for gfx950 (host only: the
+    run-time build of rt_set_jit, here for an empty scene)."""
+    assert rc.jit_compile_check("gfx950", grouped) > 1000
