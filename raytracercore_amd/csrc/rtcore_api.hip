@@ -1085,6 +1085,7 @@ int resolve_traversal(rt_scene* s)
 
 PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint64_t seed, uint64_t base);
 int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t stream);
+int prepare_jit(rt_scene* s);
 int end_op(rt_scene* s, hipStream_t stream);
 
 // AUTO on a small scene: flat or grouped brute force?  Whether a group can be skipped depends on
@@ -1806,7 +1807,9 @@ int rt_scene_set_camera(rt_scene* s, const rt_camera* cam)
         }
     }
     s->has_camera = true;
-    return calibrate_grouping(s);
+    const int rc = calibrate_grouping(s);
+    if (rc == RT_OK) (void)prepare_jit(s); // build the scene-specialised kernel now, not in a launch
+    return rc;
 }
 
 int rt_scene_set_traversal(rt_scene* s, int32_t traversal)
@@ -1817,8 +1820,9 @@ int rt_scene_set_traversal(rt_scene* s, int32_t traversal)
     }
     HIP_TRY(hipSetDevice(s->device));
     s->traversal = traversal;
-    if (traversal == RT_TRAVERSAL_AUTO && s->has_camera) return calibrate_grouping(s);
-    return resolve_traversal(s);
+    const int rc = (traversal == RT_TRAVERSAL_AUTO && s->has_camera) ? calibrate_grouping(s) : resolve_traversal(s);
+    if (rc == RT_OK && s->has_camera) (void)prepare_jit(s);
+    return rc;
 }
 
 int rt_scene_get_info(const rt_scene* s, rt_scene_info* info)

@@ -10,7 +10,8 @@ import sys
 import json
 
 d = sys.argv[1]
-sub = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].endswith(".json") else "path_kernel"
+sub = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].endswith(".json") else None  # None: either path kernel
+PATH_KERNELS = ("path_kernel", "rt_path_const")  # generic template instances, the scene-specialised build
 json_out = next((a for a in sys.argv[2:] if a.endswith(".json")), None)
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 names = {}
@@ -19,7 +20,8 @@ for f in glob.glob(os.path.join(d, "pmc*", "pmc_counter_collection.csv")):
         kname = r["Kernel_Name"]
         i = kname.find("path_kernel")
         tmpl = kname[i:].split(">")[0] if i >= 0 else ""
-        if sub in kname and not tmpl.endswith("true"):  # skip the instrumented (STATS) variant
+        hit = (sub in kname) if sub else any(k in kname for k in PATH_KERNELS)
+        if hit and not tmpl.endswith("true"):  # skip the instrumented (STATS) variant
             key = (os.path.basename(os.path.dirname(f)), int(r["Dispatch_Id"]))
             agg[key][r["Counter_Name"]] += float(r["Counter_Value"])
             names[key] = r["Kernel_Name"][:70]
