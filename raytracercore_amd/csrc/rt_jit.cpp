@@ -81,6 +81,17 @@ void write_file_atomic(const std::string& dir, const std::string& path, const st
     if (ec) std::filesystem::remove(tmp, ec);
 }
 
+// RTCORE_JIT_FLAGS: extra compiler flags for experiments (e.g. "-DRT_EXP_DUP_TRACE"), space-separated
+std::vector<std::string> jit_extra_flags()
+{
+    std::vector<std::string> out;
+    if (const char* e = std::getenv("RTCORE_JIT_FLAGS")) {
+        std::istringstream in(e);
+        for (std::string f; in >> f;) out.push_back(f);
+    }
+    return out;
+}
+
 std::string main_source(bool grouped)
 {
     return std::string("#include \"rt_jit_prelude.h\"\n#define RT_SCENE_CONST\n#define RT_SCENE_CONST_GROUPED ") +
@@ -106,9 +117,11 @@ bool compile(const std::string& arch, const std::string& main_src, const std::st
     const std::string arch_opt = "--offload-arch=" + arch;
     // the library's own kernel flags (Makefile HIPFLAGS): no fused multiply-adds the source does not
     // write, no SLP packing (v_pk_* issue no faster than two plain ops on gfx950)
-    const char* opts[] = {arch_opt.c_str(), "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
-                          "-munsafe-fp-atomics"};
-    const hiprtcResult r = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof opts[0]), opts);
+    std::vector<std::string> extra = jit_extra_flags();
+    std::vector<const char*> opts = {arch_opt.c_str(), "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
+                                     "-munsafe-fp-atomics"};
+    for (const std::string& f : extra) opts.push_back(f.c_str());
+    const hiprtcResult r = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
     if (r != HIPRTC_SUCCESS) {
         size_t n = 0;
         hiprtcGetProgramLogSize(prog, &n);
@@ -184,6 +197,7 @@ bool jit_kernel(int device, const std::string& header, bool grouped, JitKernel& 
     key = fnv1a(key, header.data(), header.size());
     const std::string main_src = main_source(grouped);
     key = fnv1a(key, main_src.data(), main_src.size());
+    for (const std::string& f : jit_extra_flags()) key = fnv1a(key, f.data(), f.size());
 
     std::lock_guard<std::mutex> lock(g_mu);
     out = JitKernel{};
