@@ -671,7 +671,7 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
 #define RT_GROUPED_WAVES 7 // the same for the grouped brute-force kernel
 #endif
 #ifndef RT_WIDE_STACK
-#define RT_WIDE_STACK 24 // LDS entries of the wide BVH kernel's traversal stack (then global overflow)
+#define RT_WIDE_STACK 20 // LDS entries of the wide BVH kernel's traversal stack (then global overflow)
 #endif
 #ifndef RT_BVH_SPEC
 #define RT_BVH_SPEC 1 // speculative BVH traversal with wave-wide leaf steps (p.spec); 0: the mixed-step loop (C4 69.8 -> 62.1 ms)
@@ -683,7 +683,9 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
 #define RT_LEAF_STEP 2 // leaf primitives tested per BVH traversal step
 #endif
 #ifndef RT_BVH_WAVES
-#define RT_BVH_WAVES 5 // the same for the BVH kernels (C4: 4 waves with a 40-entry LDS stack 80.7 ms, 5 waves with 24 entries 72.0 ms)
+#define RT_BVH_WAVES 6 // the same for the BVH kernels (C4: 4 waves with a 40-entry LDS stack 80.7 ms, 5 waves with 24 entries
+                       // 72.0 ms; with the launch record read at use, 6 waves with 20 entries (8 VGPRs spilled) 57.2-58.6
+                       // against 60.7-61.3 ms at 5 / 24; 7 waves with 16 entries spill 27 VGPRs: 70.1 ms)
 #endif
 
 // LDS staging of the shading records (PrimF per slot, MatF per ID, XformF): the per-lane gathers
@@ -1022,31 +1024,28 @@ __global__ void __launch_bounds__(256, CULL ? RT_GROUPED_WAVES : RT_PATH_WAVES)
 // paid once per batch of finished queries.
 template <int WIDTH, int STACK, bool LDS, bool STATS>
 __global__ void __launch_bounds__(256, RT_BVH_WAVES)
-    path_kernel_bvh(PathScene s, const CameraF* __restrict__ camp, const PathParams* __restrict__ pp,
-                    const TestRec* __restrict__ tests,
-                    const RectRec* __restrict__ rects, const FrameRec* __restrict__ frames,
-                    const PrimF* __restrict__ prims_g,
-                    const NodeF* __restrict__ nodes, const Node4Q* __restrict__ nodes4,
-                    const GroupRec* __restrict__ groups, const XformF* __restrict__ xf,
-                    const MatF* __restrict__ mats_g, const float4* __restrict__ vnormals)
+    path_kernel_bvh(PathScene, const CameraF* __restrict__ camp, const PathParams* __restrict__ pp, const TestRec*,
+                    const RectRec*, const FrameRec*, const PrimF*, const NodeF*, const Node4Q*, const GroupRec*,
+                    const XformF*, const MatF*, const float4*)
 {
-    const PathParams p = *pp;
+    // As in the brute-force kernels, the camera and the launch record are read through opaque
+    // constant-address-space pointers where they are used (held whole-kernel in SGPRs, they
+    // spilled 58 SGPRs into VGPR lanes here); the other arguments are unused.
+    const ParamsC& P0 = *(const ParamsC*)pp;
     __shared__ int stack_mem[STACK * 256];
     extern __shared__ float4 lds_scene[];
-    const TravStack stk{stack_mem + threadIdx.x, p.stack_ovf + blockIdx.x * 256 + threadIdx.x, (int)gridDim.x * 256};
-    const CameraF cam = *camp;
-    const ShadeRecs R = stage_scene<LDS>(s, prims_g, mats_g, xf, lds_scene);
+    const TravStack stk{stack_mem + threadIdx.x, P0.stack_ovf + blockIdx.x * 256 + threadIdx.x, (int)gridDim.x * 256};
+    const ShadeRecs R = stage_scene<LDS>(P0.scene, P0.prims, P0.mats, P0.xf, lds_scene);
     // hot wide nodes after the staged shading records (dynamic LDS; see path_lds_bytes)
-    Node4Q* lds_hot = reinterpret_cast<Node4Q*>(lds_scene + (LDS ? scene_lds_float4s(s) : 0));
-    if (WIDTH == 4 && s.n_hot4 > 0) {
-        const float4* src = reinterpret_cast<const float4*>(s.hot4);
+    Node4Q* lds_hot = reinterpret_cast<Node4Q*>(lds_scene + (LDS ? scene_lds_float4s(P0.scene) : 0));
+    if (WIDTH == 4 && P0.scene.n_hot4 > 0) {
+        const float4* src = reinterpret_cast<const float4*>(P0.scene.hot4);
         float4* dst = reinterpret_cast<float4*>(lds_hot);
-        for (int i = threadIdx.x; i < s.n_hot4 * 4; i += blockDim.x) dst[i] = src[i];
+        for (int i = threadIdx.x; i < P0.scene.n_hot4 * 4; i += blockDim.x) dst[i] = src[i];
         __syncthreads();
     }
     const int lane = threadIdx.x & 63;
-    const unsigned total = (unsigned)p.n_chunks * (unsigned)p.n_pad;
-    const int pln0 = s.n_bvh;
+    const unsigned total = (unsigned)P0.n_chunks * (unsigned)P0.n_pad;
     Lane L;
     lane_init(L);
     Sample S;
@@ -1062,17 +1061,31 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
     Best b{__builtin_huge_valf(), -1};
 
     while (true) {
+        const ParamsC* pq = (const ParamsC*)pp;
+        asm volatile("" : "+s"(pq));
+        const CameraC* cp = (const CameraC*)camp;
+        asm volatile("" : "+s"(cp));
+        const ParamsC& p = *pq;
+        const auto& s = pq->scene;
+        const auto tests = (const RT_AS_CONST TestRec*)pq->tests;
+        const auto xf = (const RT_AS_CONST XformF*)pq->xf;
+        const auto vnormals = (const RT_AS_CONST float4*)pq->vnormals;
+        const auto nodes = (const RT_AS_CONST NodeF*)pq->nodes;
+        const auto nodes4 = (const RT_AS_CONST Node4Q*)pq->nodes4;
         const unsigned long long waiting = __ballot(!trav && (L.active || L.live));
         const unsigned long long busy = __ballot(trav);
         if (!waiting && !busy) break;
         if (!busy || __popcll(waiting) >= p.refill) {
             wave_rays += (unsigned)__popcll(__ballot(done)); // one Scene.RayTrace per finished query
             if (done) { // the query finished: planes (outside the BVH), then one bounce
-                for (int i = pln0; i < pln0 + s.n_pln; i++) hit_plane(tests[i], i, S.o, S.d, S.prev, b);
+                for (int i = s.n_bvh; i < s.n_bvh + s.n_pln; i++) {
+                    const TestRec tr = tests[i];
+                    hit_plane(tr, i, S.o, S.d, S.prev, b);
+                }
                 bounce(L, S, s, R, vnormals, tests, b);
                 done = false;
             }
-            refill(L, S, p, s, cam, lane, total);
+            refill(L, S, p, s, *cp, lane, total);
             if (L.live && !trav) { // start the next query
                 id = v3(slab_rcp(S.d.x), slab_rcp(S.d.y), slab_rcp(S.d.z));
                 oi = S.o * id;
@@ -1119,7 +1132,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
             } else if (can_node) {
                 bool pop = true;
                 if (WIDTH == 4) {
-                    const Node4Q q = (ref & RT_HOT_BIT) ? lds_hot[ref & ~RT_HOT_BIT] : nodes4[ref];
+                    const Node4Q q = (ref & RT_HOT_BIT) ? lds_hot[ref & ~RT_HOT_BIT] : Node4Q(nodes4[ref]);
                     wide_visit<STACK>(q, id, oi, b.t, ref, sp, stk, pop);
                 } else {
                     const NodeF n = nodes[ref];
@@ -1183,7 +1196,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                 pop = k >= kend;
             } else if (WIDTH == 4) {
                 // the top of the tree comes from LDS, the rest from global memory
-                const Node4Q q = (ref & RT_HOT_BIT) ? lds_hot[ref & ~RT_HOT_BIT] : nodes4[ref];
+                const Node4Q q = (ref & RT_HOT_BIT) ? lds_hot[ref & ~RT_HOT_BIT] : Node4Q(nodes4[ref]);
                 wide_visit<STACK>(q, id, oi, b.t, ref, sp, stk, pop);
                 if (STATS) cnt.nodes++;
             } else {
@@ -1227,7 +1240,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
             }
         }
     }
-    flush_counts<STATS>(wave_rays, cnt, p, lane);
+    flush_counts<STATS>(wave_rays, cnt, P0, lane);
 }
 
 #ifndef __HIPCC_RTC__ // the host side and the other kernels (not part of a hiprtc build)
@@ -1324,7 +1337,7 @@ PathKernel pick_bvh(bool stats)
 }
 
 // variant = kernel * 2 + lds; kernel 0 brute force (flat), 1 brute force (grouped, culled),
-// 2 BVH2 (24-entry LDS stack), 3 wide BVH (40-entry LDS stack); both stacks overflow to global memory
+// 2 BVH2 (24-entry LDS stack), 3 wide BVH (RT_WIDE_STACK-entry LDS stack); both overflow to global memory
 PathKernel pick(int variant, bool stats)
 {
     switch (variant) {
@@ -1423,6 +1436,8 @@ void fill_launch(const DevScene& s, int variant, PathParams& p)
     p.frames = grouped ? s.frames_gr : s.frames_bf;
     p.prims = bvh ? s.prims_bvh : grouped ? s.prims_gr : s.prims_bf;
     p.groups = grouped ? s.groups_gr : s.groups_bf;
+    p.nodes = s.nodes;
+    p.nodes4 = s.nodes4;
     p.xf = s.xf;
     p.mats = s.mats;
     p.vnormals = s.vnormals;

@@ -41,6 +41,8 @@ struct PathParams {
     const FrameRec* frames;
     const PrimF* prims;
     const GroupRec* groups;
+    const NodeF* nodes;         // BVH kernels: the BVH2 and the wide tree
+    const Node4Q* nodes4;
     const XformF* xf;
     const MatF* mats;
     const float4* vnormals;

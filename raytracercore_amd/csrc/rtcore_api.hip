@@ -937,7 +937,7 @@ int upload_scene(rt_scene* s)
     std::vector<Node4Q> hot;
     int root4_hot = s->bvh.root4;
     {
-        int k_hot = 64; // with the 24-entry LDS stack: 5 blocks x (24 + 4) KB per CU
+        int k_hot = 64; // with the 20-entry LDS stack: 6 blocks x (20 + 4) KB per CU
         if (const char* e = getenv("RTCORE_HOT_NODES")) k_hot = std::max(0, std::min(1024, atoi(e)));
         if (k_hot > 0 && s->bvh.root4 >= 0 && s->bvh.n_nodes4 > 0) {
             std::vector<Node4Q> all4((size_t)s->bvh.n_nodes4);
