@@ -1147,8 +1147,13 @@ PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint6
     p.band = 0;
     p.spp = spp;
     // a few chunks per pixel keep the tail of a launch short while each lane still amortises
-    // its item fetch over many samples (RTCORE_PATH_CHUNKS overrides the count, for tuning)
+    // its item fetch over many samples (RTCORE_PATH_CHUNKS overrides the count, for tuning).
+    // A launch over fewer pixels than a 1080p frame takes proportionally more chunks per pixel
+    // (up to 256), so that a band set of 1/N of the frame at N x the samples (bench.py on N GPUs)
+    // gets items as short as one GPU's whole-frame launch, and with them the same launch tail.
     int chunks = 32;
+    const double npix = (double)w * (double)h;
+    if (npix > 0 && npix < 2073600.0) chunks = (int)std::min(256.0, 32.0 * std::ceil(2073600.0 / npix));
     if (const char* e = getenv("RTCORE_PATH_CHUNKS")) chunks = std::max(1, atoi(e));
     p.chunk = std::max(1, std::min(64, (spp + chunks - 1) / chunks));
     const int used = (spp + p.chunk - 1) / p.chunk;
