@@ -1232,7 +1232,11 @@ int prepare_jit(rt_scene* s)
     }
     const bool grouped = s->variant == path_variant(1, true);
     const unsigned gen = grouped ? s->group_order_gen : 0;
-    if (s->jit.variant == s->variant && s->jit.gen == gen) return s->jit.fn ? 1 : 0;
+    if (s->jit.variant == s->variant && s->jit.gen == gen) { // built (or failed) already
+        s->jit.status = s->jit.fn ? 1 : (s->jit.error.empty() ? 0 : -1);
+        return s->jit.fn ? 1 : 0;
+    }
+    s->jit.error.clear();
     s->jit.variant = s->variant;
     s->jit.gen = gen;
     s->jit.fn = nullptr;
