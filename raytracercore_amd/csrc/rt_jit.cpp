@@ -203,6 +203,18 @@ bool jit_kernel(int device, const std::string& header, bool grouped, JitKernel& 
     out = JitKernel{};
     Entry& e = g_cache[{device, key}];
     if (!e.mod) {
+        // the module belongs to the device's context: load it there whatever device is current
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        struct Restore {
+            int dev;
+            ~Restore() { (void)hipSetDevice(dev); }
+        } restore{cur};
+        if (hipSetDevice(device) != hipSuccess) {
+            err = "hipSetDevice failed";
+            g_cache.erase({device, key});
+            return false;
+        }
         char hex[32];
         std::snprintf(hex, sizeof hex, "%016llx", (unsigned long long)key);
         const std::string dir = cache_dir(), path = dir + "/" + hex + ".co";
