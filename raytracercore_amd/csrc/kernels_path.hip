@@ -259,6 +259,9 @@ __device__ __forceinline__ void trace_brute(const SceneT& s, GroupP groups, Test
     const V3 id = v3(slab_rcp(d.x), slab_rcp(d.y), slab_rcp(d.z));
     const V3 oi = o * id;
     const int n_groups = CULL ? s.n_groups : 1; // the flat order is one group (1/d and o/d die after its rects)
+#ifdef RT_SCENE_CONST
+#pragma unroll // the scene-specialised build: every group's tests in line, their records literals
+#endif
     for (int g = 0; g < n_groups; g++) {
         const GroupRec G = groups[g];
         if (CULL) {

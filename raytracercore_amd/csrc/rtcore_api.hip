@@ -1220,10 +1220,12 @@ int check_tile(rt_scene* s, int x0, int y0, int w, int h)
 // (the generic kernel computes the same; the failure is kept in s->jit.error).
 int prepare_jit(rt_scene* s)
 {
-    // The flat order only by default: unrolled in full, the grouped order's culled group loop ran
-    // slower (die.txt C3 36.6 -> 37.9 ms), presumably from the code size; RTCORE_JIT_GROUPED=1 builds it.
+    // Both brute-force orders (RTCORE_JIT_GROUPED=0 leaves the grouped one generic).  The grouped
+    // order's group loop is unrolled by pragma: left to the compiler's heuristics it stayed a loop
+    // over constant memory and ran slower than the generic kernel (die.txt 36.6 -> 37.9 ms);
+    // unrolled, die.txt C3 36.6 -> 30.9 ms.
     const char* eg = getenv("RTCORE_JIT_GROUPED");
-    const bool grouped_ok = eg && eg[0] == '1';
+    const bool grouped_ok = !(eg && eg[0] == '0');
     const bool eligible = jit_enabled() && !s->stats_on &&
                           (s->variant == path_variant(0, true) || (grouped_ok && s->variant == path_variant(1, true)));
     if (!eligible) {

@@ -10,7 +10,6 @@
   Recursion + 1.
 """
 import ctypes as C
-import os
 
 import numpy as np
 import pytest
@@ -611,7 +610,6 @@ def test_scene_specialised_kernel_matches_generic(rc, scenes, name, mode):
         scene = scenes[name]
     trav = getattr(rc, "RT_TRAVERSAL_" + mode)
     out = {}
-    os.environ["RTCORE_JIT_GROUPED"] = "1"  # the grouped order's build is opt-in (slower on die.txt)
     try:
         for on in (True, False):
             rc.set_jit(on)
@@ -622,7 +620,6 @@ def test_scene_specialised_kernel_matches_generic(rc, scenes, name, mode):
             g.close()
     finally:
         rc.set_jit(True)
-        del os.environ["RTCORE_JIT_GROUPED"]
     (sa, na, ma, ra), (sb, nb, mb, rb) = out[True], out[False]
     assert ra == rb and np.array_equal(na, nb) and np.array_equal(ma, mb)
     assert np.array_equal(sa, sb)
@@ -630,14 +627,6 @@ def test_scene_specialised_kernel_matches_generic(rc, scenes, name, mode):
 
 def test_scene_specialised_kernel_follows_camera_group_order(rc, scenes):
     """Grouped order: the groups are re-sorted per camera, and the specialised build follows."""
-    os.environ["RTCORE_JIT_GROUPED"] = "1"
-    try:
-        _grouped_camera_switch(rc, scenes)
-    finally:
-        del os.environ["RTCORE_JIT_GROUPED"]
-
-
-def _grouped_camera_switch(rc, scenes):
     g = rc.GpuRaytracer(scenes["die.txt"], 0, size=(64, 48), traversal=rc.RT_TRAVERSAL_GROUPED)
     a0 = g.render_tile(0, 0, 64, 48, 8, seed=3)
     cam2 = rc.rt_camera.from_buffer_copy(scenes["die.txt"].cameras[2])
