@@ -935,7 +935,11 @@ __device__ __forceinline__ void path_body(const CameraF* __restrict__ camp, cons
 #else
         const auto& sc = pq->scene;
 #endif
+#ifdef RT_SCENE_CONST
+        refill(L, S, *pq, sc, *(const CameraF*)kCameraW, lane, total); // the camera compiled in too
+#else
         refill(L, S, *pq, sc, *cp, lane, total);
+#endif
         if (!__any(L.active)) break;
         if (STATS) t1 = __builtin_readcyclecounter();
 #ifdef RT_EXP_DUP_START // cost experiment: a second camera sample on a copy

@@ -163,7 +163,7 @@ bool jit_enabled()
 
 void jit_set_enabled(bool on) { g_jit.store(on ? 1 : 0); }
 
-std::string jit_scene_header(const PathScene& ps, const std::vector<GroupRec>& groups,
+std::string jit_scene_header(const PathScene& ps, const CameraF& cam, const std::vector<GroupRec>& groups,
                              const std::vector<RectRec>& rects, const std::vector<FrameRec>& frames,
                              const std::vector<TestRec>& tests, const std::vector<XformF>& xf)
 {
@@ -174,6 +174,7 @@ std::string jit_scene_header(const PathScene& ps, const std::vector<GroupRec>& g
     p.n_hot4 = 0;
     p.width = 0;      // read from the launch record (one build serves every frame size)
     put_words(o, "kSceneW", std::vector<PathScene>{p});
+    put_words(o, "kCameraW", std::vector<CameraF>{cam});
     put_words(o, "kGroupsW", groups);
     put_words(o, "kRectsW", rects);
     put_words(o, "kFramesW", frames);
@@ -246,7 +247,7 @@ bool jit_kernel(int device, const std::string& header, bool grouped, JitKernel& 
 
 size_t jit_compile_check(const std::string& arch, bool grouped, std::string& err)
 {
-    const std::string header = jit_scene_header(PathScene{}, {}, {}, {}, {}, {});
+    const std::string header = jit_scene_header(PathScene{}, CameraF{}, {}, {}, {}, {}, {});
     std::vector<char> code;
     if (!compile(arch, main_source(grouped), header, code, err)) return 0;
     return code.size();

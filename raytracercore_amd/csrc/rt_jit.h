@@ -15,8 +15,9 @@
 
 namespace rtc {
 
-// The generated header (kSceneW, kGroupsW, kRectsW, kFramesW, kTestsW, kXfW) of one launch.
-std::string jit_scene_header(const PathScene& ps, const std::vector<GroupRec>& groups,
+// The generated header (kSceneW, kCameraW, kGroupsW, kRectsW, kFramesW, kTestsW, kXfW) of one
+// scene, camera and slot order.
+std::string jit_scene_header(const PathScene& ps, const CameraF& cam, const std::vector<GroupRec>& groups,
                              const std::vector<RectRec>& rects, const std::vector<FrameRec>& frames,
                              const std::vector<TestRec>& tests, const std::vector<XformF>& xf);
 

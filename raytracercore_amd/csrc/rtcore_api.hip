@@ -137,7 +137,7 @@ struct rt_scene {
         std::vector<TestRec> tests;
     } flat_h, grouped_h;
     std::vector<XformF> xf_h;
-    unsigned group_order_gen = 0; // bumped when the grouped order's group order changes
+    unsigned jit_gen = 0; // bumped by every camera change (and with it the grouped order's group order)
     struct {
         int variant = -1;          // the variant and group order the function was built for
         unsigned gen = 0;
@@ -1233,7 +1233,7 @@ int prepare_jit(rt_scene* s)
         return 0;
     }
     const bool grouped = s->variant == path_variant(1, true);
-    const unsigned gen = grouped ? s->group_order_gen : 0;
+    const unsigned gen = s->jit_gen;
     if (s->jit.variant == s->variant && s->jit.gen == gen) { // built (or failed) already
         s->jit.status = s->jit.fn ? 1 : (s->jit.error.empty() ? 0 : -1);
         return s->jit.fn ? 1 : 0;
@@ -1245,7 +1245,7 @@ int prepare_jit(rt_scene* s)
     PathParams lp{};
     fill_launch(s->dev, s->variant, lp);
     const auto& B = grouped ? s->grouped_h : s->flat_h;
-    const std::string header = jit_scene_header(lp.scene, B.groups, B.rects, B.frames, B.tests, s->xf_h);
+    const std::string header = jit_scene_header(lp.scene, s->camf, B.groups, B.rects, B.frames, B.tests, s->xf_h);
     if (const char* dump = getenv("RTCORE_JIT_DUMP")) { // inspection: the generated header of the last build
         if (FILE* f = fopen(dump, "w")) {
             fwrite(header.data(), 1, header.size(), f);
@@ -1812,12 +1812,10 @@ int rt_scene_set_camera(rt_scene* s, const rt_camera* cam)
         };
         std::stable_sort(g.begin(), g.end(), [&](const GroupRec& a, const GroupRec& b) { return dist2(a) < dist2(b); });
         HIP_TRY(hipMemcpy(s->groups_gr.p, g.data(), g.size() * sizeof(GroupRec), hipMemcpyHostToDevice));
-        if (memcmp(g.data(), s->grouped_h.groups.data(), g.size() * sizeof(GroupRec)) != 0) {
-            s->grouped_h.groups = g;
-            s->group_order_gen++;
-        }
+        s->grouped_h.groups = g; // the order the scene-specialised grouped kernel is built with
     }
     s->has_camera = true;
+    s->jit_gen++; // the scene-specialised kernel carries the camera (and the group order)
     const int rc = calibrate_grouping(s);
     if (rc == RT_OK) (void)prepare_jit(s); // build the scene-specialised kernel now, not in a launch
     return rc;
