@@ -321,6 +321,10 @@ def main() -> int:
                        "traversal": ["auto", "brute", "bvh4", "bvh2", "grouped"][info.traversal], "recursion": scene.params.recursion,
                        "parallelism": parallelism},
             "samples_per_s": round(total_samples / elapsed, 1),
+            # the reference's only published figure: 6.240 spp/s at 700x700 on bounce.txt,
+            # i.e. 3.06 M camera samples/s, on an unknown ~32-thread CPU; a different metric from
+            # Mrays/s, so vs_baseline stays null
+            "published_reference": {"samples_per_s": 3.0576e6, "source": "Screenshots/app.png status bar"},
             "rays_per_sample": round(total_rays / total_samples, 4),
             "kernel_ms": round(avg_ms, 3),
             "roofline": roofline(args.config, fpr, bpr, my_rays_per_step, avg_ms),
