@@ -641,3 +641,24 @@ def test_scene_specialised_kernel_follows_camera_group_order(rc, scenes):
         rc.set_jit(True)
     assert a2[3] == b2[3] and np.array_equal(a2[0], b2[0]) and np.array_equal(a2[1], b2[1])
     assert not np.array_equal(a0[0], a2[0])
+
+
+def test_scene_specialised_build_failure_falls_back(rc, scenes, monkeypatch):
+    """A failing run-time build (here: a bad compiler flag) leaves the generic kernel in charge:
+    the render is unchanged, build statistic 15 reads -1 and rt_scene_get_jit_error says why."""
+    monkeypatch.setenv("RTCORE_JIT_FLAGS", "-DRT_JIT_BROKEN_FLAG=( -include rt_no_such_header.h")
+    g = rc.GpuRaytracer(scenes["bounce.txt"], 0, size=(48, 32), traversal=rc.RT_TRAVERSAL_BRUTE)
+    a = g.render_tile(0, 0, 48, 32, 8, seed=2)
+    st = g.build_stats()
+    err = g.jit_error()
+    g.close()
+    assert st["jit_status"] == -1.0 and "hiprtc" in err
+    monkeypatch.delenv("RTCORE_JIT_FLAGS")
+    rc.set_jit(False)
+    try:
+        h = rc.GpuRaytracer(scenes["bounce.txt"], 0, size=(48, 32), traversal=rc.RT_TRAVERSAL_BRUTE)
+        b = h.render_tile(0, 0, 48, 32, 8, seed=2)
+        h.close()
+    finally:
+        rc.set_jit(True)
+    assert a[3] == b[3] and np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
