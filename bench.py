@@ -319,6 +319,7 @@ def main() -> int:
             "data": "synthetic: the reference's own scene file (tests/golden/scenes) with seeded camera samples",
             "config": {"workload": f"{scene_file} camera {cam} {W}x{H} x {spp} spp per GPU per step",
                        "traversal": ["auto", "brute", "bvh4", "bvh2", "grouped"][info.traversal], "recursion": scene.params.recursion,
+                       "kernel_build": "scene-specialised (hiprtc)" if build.get("jit_status") == 1.0 else "generic",
                        "parallelism": parallelism},
             "samples_per_s": round(total_samples / elapsed, 1),
             # the reference's only published figure: 6.240 spp/s at 700x700 on bounce.txt,
