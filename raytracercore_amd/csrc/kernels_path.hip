@@ -558,7 +558,7 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
     const PrimF P = prims[b.sg >> 1];
     const uint32_t fl = __float_as_uint(P.b.w);
     const int id = __float_as_int(P.a.w);
-    const MatF& M = mats[id];
+    const MatF& M = mats[__float_as_int(P.d.w)]; // the primitive's material (deduplicated table)
     const uint32_t kind = fl & KIND_MASK;
     const V3 emis = xyz(M.emission);
     if (s.debug_geom) { // Raytracer.cs:93-98
@@ -703,7 +703,7 @@ __device__ __forceinline__ ShadeRecs stage_scene(const SceneT& s, const PrimF* p
                                                  const XformF* xf, float4* lds_scene)
 {
     if (!LDS) return ShadeRecs{prims_g, mats_g, xf};
-    const int n_p = s.n_slots * (int)(sizeof(PrimF) / 16), n_m = s.n_ids * (int)(sizeof(MatF) / 16),
+    const int n_p = s.n_slots * (int)(sizeof(PrimF) / 16), n_m = s.n_mats * (int)(sizeof(MatF) / 16),
               n_x = s.n_xf * (int)(sizeof(XformF) / 16);
     const float4* gp = reinterpret_cast<const float4*>(prims_g);
     const float4* gm = reinterpret_cast<const float4*>(mats_g);
@@ -718,7 +718,7 @@ __device__ __forceinline__ ShadeRecs stage_scene(const SceneT& s, const PrimF* p
 
 __device__ __forceinline__ int scene_lds_float4s(const PathScene& s)
 {
-    return s.n_slots * (int)(sizeof(PrimF) / 16) + s.n_ids * (int)(sizeof(MatF) / 16) +
+    return s.n_slots * (int)(sizeof(PrimF) / 16) + s.n_mats * (int)(sizeof(MatF) / 16) +
            s.n_xf * (int)(sizeof(XformF) / 16);
 }
 
@@ -1368,7 +1368,7 @@ PathScene make_path_scene(const DevScene& s)
     ps.n_pln = s.n_pln;
     ps.n_bvh = s.pln0_bf; // set per order by launch_path
     ps.n_slots = ps.n_bvh + s.n_pln;
-    ps.n_ids = s.n_ids;
+    ps.n_mats = s.n_mats;
     ps.n_xf = s.n_xf;
     ps.root = s.root;
     ps.width = s.width;
@@ -1391,7 +1391,7 @@ int path_wide_stack() { return RT_WIDE_STACK; }
 size_t path_lds_bytes(const DevScene& s)
 {
     const size_t slots = (size_t)std::max(std::max(s.pln0_bf, s.pln0_gr), s.pln0_bvh) + s.n_pln;
-    return slots * sizeof(PrimF) + (size_t)s.n_ids * sizeof(MatF) + (size_t)s.n_xf * sizeof(XformF);
+    return slots * sizeof(PrimF) + (size_t)s.n_mats * sizeof(MatF) + (size_t)s.n_xf * sizeof(XformF);
 }
 
 int path_variant(int kernel, bool lds) { return kernel * 2 + (lds ? 1 : 0); }

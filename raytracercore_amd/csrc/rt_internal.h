@@ -112,7 +112,7 @@ struct alignas(16) XformF {     // rows 0-2 (last row is 0 0 0 1)
                                 // MatrixToNormal * (MatrixToWorld * p - centre) / r (Sphere.cs:50-155)
 };
 
-struct alignas(16) MatF {       // per primitive ID, 80 B
+struct alignas(16) MatF {       // one per distinct material (PrimF.d.w indexes it), 80 B
     float4 emission;            // rgb, luminance
     float4 diffuse;             // rgb, luminance
     float4 specular;            // rgb (Shininess<=0 -> black), luminance
@@ -162,7 +162,7 @@ struct PathScene {
     int32_t n_tri, n_sph, n_pln;
     int32_t n_bvh;               // primitives in the BVH (all but planes); planes follow them
     int32_t n_slots;             // n_bvh + n_pln (PrimF records)
-    int32_t n_ids;               // primitive IDs (MatF records)
+    int32_t n_mats;              // MatF records (distinct materials)
     int32_t n_xf;                // XformF records
     int32_t n_groups;            // brute force: GroupRec records
     int32_t root;                // child reference of the BVH root
@@ -303,7 +303,7 @@ struct DevScene {
     const XformF* xf;
     const MatF* mats;
     const float4* vnormals;     // 3 per primitive ID (HasNormals triangles)
-    int32_t n_ids;              // MatF records
+    int32_t n_mats;             // MatF records (distinct materials)
     int32_t n_xf;               // XformF records
     // exact set
     const PrimD* prims_d;

@@ -838,6 +838,48 @@ int upload_scene(rt_scene* s)
         s->layout.tris = L.tris;
         s->layout.sphs = L.sphs;
     }
+    // Materials, deduplicated: one MatF per distinct record, PrimF.d.w its index.  A 1M-triangle
+    // mesh of one material then shades from a table of a few records (cache-resident) instead of
+    // gathering 80 B per hit from an 80 MB per-primitive array.
+    std::vector<MatF> mats;
+    std::vector<int32_t> mat_of(n);
+    std::unordered_map<std::string, int32_t> mat_index;
+    for (int i = 0; i < n; i++) {
+        const HostPrim& p = H[i];
+        const bool refl = p.shininess > 0; // Primitive.IsReflective (Primitive.cs:107-129)
+        rt_color spec = refl ? p.specular : rt_color{0, 0, 0};
+        rt_color refr = refl ? p.refraction : rt_color{0, 0, 0};
+        MatF m;
+        std::memset(&m, 0, sizeof m);
+        m.emission = make_float4((float)p.emission.r, (float)p.emission.g, (float)p.emission.b, (float)luminance(p.emission));
+        m.diffuse = make_float4((float)p.diffuse.r, (float)p.diffuse.g, (float)p.diffuse.b, (float)luminance(p.diffuse));
+        m.specular = make_float4((float)spec.r, (float)spec.g, (float)spec.b, (float)luminance(spec));
+        m.refraction = make_float4((float)refr.r, (float)refr.g, (float)refr.b, (float)luminance(refr));
+        m.shininess = (float)p.shininess;
+        m.ior = (float)p.ior;
+        m.flags = p.flags;
+        m.inv_shininess = (float)(1.0 / p.shininess);
+        // Raytracer.cs:127-133: ratio = iorIn / iorOut, air outside, swapped when the hit is Inside
+        m.eta_enter = p.ior != 0 ? (float)(s->params.air_ior / p.ior) : 0.0f;
+        m.eta_exit = p.ior != 0 ? (float)(p.ior / s->params.air_ior) : 0.0f;
+        m.pad[0] = m.pad[1] = 0.0f;
+        const std::string key(reinterpret_cast<const char*>(&m), sizeof m);
+        auto it = mat_index.find(key);
+        if (it == mat_index.end()) {
+            it = mat_index.emplace(key, (int32_t)mats.size()).first;
+            mats.push_back(m);
+        }
+        mat_of[i] = it->second;
+    }
+    auto set_mats = [&](std::vector<PrimF>& v) { // PrimF.d.w = the material of the record's ID
+        for (PrimF& f : v) {
+            int32_t id;
+            std::memcpy(&id, &f.a.w, 4);
+            f.d.w = as_f(mat_of[id]);
+        }
+    };
+    set_mats(flat.prims);
+    set_mats(grouped.prims);
     std::vector<PrimF> bv;
     std::vector<TestRec> tbv;
     size_t n_bvh_records = 0;
@@ -858,6 +900,7 @@ int upload_scene(rt_scene* s)
             HIP_TRY(hipMemcpy(s->order_d.p + nb, planes.data(), planes.size() * sizeof(int32_t), hipMemcpyHostToDevice));
         DevBuf<PrimF> pid_d;
         DevBuf<TestRec> tid_d;
+        set_mats(pid);
         HIP_TRY(pid_d.upload(pid));
         HIP_TRY(tid_d.upload(tid));
         HIP_TRY(s->prims_bvh.reserve(n_bvh_records));
@@ -880,26 +923,7 @@ int upload_scene(rt_scene* s)
             }
         n_bvh_records = bv.size();
     }
-    std::vector<MatF> mats(n);
-    for (int i = 0; i < n; i++) {
-        const HostPrim& p = H[i];
-        const bool refl = p.shininess > 0; // Primitive.IsReflective (Primitive.cs:107-129)
-        rt_color spec = refl ? p.specular : rt_color{0, 0, 0};
-        rt_color refr = refl ? p.refraction : rt_color{0, 0, 0};
-        MatF& m = mats[i];
-        m.emission = make_float4((float)p.emission.r, (float)p.emission.g, (float)p.emission.b, (float)luminance(p.emission));
-        m.diffuse = make_float4((float)p.diffuse.r, (float)p.diffuse.g, (float)p.diffuse.b, (float)luminance(p.diffuse));
-        m.specular = make_float4((float)spec.r, (float)spec.g, (float)spec.b, (float)luminance(spec));
-        m.refraction = make_float4((float)refr.r, (float)refr.g, (float)refr.b, (float)luminance(refr));
-        m.shininess = (float)p.shininess;
-        m.ior = (float)p.ior;
-        m.flags = p.flags;
-        m.inv_shininess = (float)(1.0 / p.shininess);
-        // Raytracer.cs:127-133: ratio = iorIn / iorOut, air outside, swapped when the hit is Inside
-        m.eta_enter = p.ior != 0 ? (float)(s->params.air_ior / p.ior) : 0.0f;
-        m.eta_exit = p.ior != 0 ? (float)(p.ior / s->params.air_ior) : 0.0f;
-        m.pad[0] = m.pad[1] = 0.0f;
-    }
+    set_mats(bv);
     HIP_TRY(s->prims_d.upload(pd));
     HIP_TRY(s->xf_d.upload(xd));
     HIP_TRY(s->prims_bf.upload(flat.prims));
@@ -1010,7 +1034,7 @@ int upload_scene(rt_scene* s)
     d.xf = s->xf.p;
     d.mats = s->mats.p;
     d.vnormals = s->vnormals.p;
-    d.n_ids = n;
+    d.n_mats = (int)mats.size();
     d.n_xf = (int)xf.size();
     d.prims_d = s->prims_d.p;
     d.xf_d = s->xf_d.p;
