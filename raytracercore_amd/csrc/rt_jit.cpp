@@ -219,24 +219,41 @@ bool jit_kernel(int device, const std::string& header, bool grouped, JitKernel& 
         char hex[32];
         std::snprintf(hex, sizeof hex, "%016llx", (unsigned long long)key);
         const std::string dir = cache_dir(), path = dir + "/" + hex + ".co";
+        auto load = [&](const std::vector<char>& code) {
+            if (hipModuleLoadData(&e.mod, code.data()) == hipSuccess &&
+                hipModuleGetFunction(&e.fn, e.mod, "rt_path_const") == hipSuccess)
+                return true;
+            if (e.mod) (void)hipModuleUnload(e.mod);
+            e = Entry{};
+            return false;
+        };
         std::vector<char> code;
+        bool loaded = false;
         if (read_file(path, code)) {
-            out.from_cache = true;
-        } else {
+            loaded = load(code);
+            if (loaded) {
+                out.from_cache = true;
+            } else {
+                // an unusable cache file (another ROCm, a damaged disk): drop it and rebuild
+                std::error_code ec;
+                std::filesystem::remove(path, ec);
+                (void)hipGetLastError();
+            }
+        }
+        if (!loaded) {
             const auto t0 = std::chrono::steady_clock::now();
             if (!compile(arch, main_src, header, code, err)) {
                 g_cache.erase({device, key});
                 return false;
             }
             out.compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            if (!load(code)) {
+                err = "loading the scene-specialised module failed";
+                (void)hipGetLastError();
+                g_cache.erase({device, key});
+                return false;
+            }
             write_file_atomic(dir, path, code);
-        }
-        if (hipModuleLoadData(&e.mod, code.data()) != hipSuccess ||
-            hipModuleGetFunction(&e.fn, e.mod, "rt_path_const") != hipSuccess) {
-            err = "loading the scene-specialised module failed";
-            if (e.mod) (void)hipModuleUnload(e.mod);
-            g_cache.erase({device, key});
-            return false;
         }
     } else {
         out.from_cache = true;

@@ -10,6 +10,7 @@
   Recursion + 1.
 """
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -662,3 +663,49 @@ def test_scene_specialised_build_failure_falls_back(rc, scenes, monkeypatch):
     finally:
         rc.set_jit(True)
     assert a[3] == b[3] and np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+_CACHE_PROBE = r"""
+import json, sys
+import numpy as np
+import raytracercore_amd as rc
+g = rc.GpuRaytracer(rc.SceneLoader.from_file(rc.scene_path("bounce.txt")), 0, size=(48, 32),
+                    traversal=rc.RT_TRAVERSAL_BRUTE)
+s = g.render_tile(0, 0, 48, 32, 4, seed=3)
+st = g.build_stats()
+print(json.dumps({"status": st["jit_status"], "cached": st["jit_cached"], "rays": int(s[3]),
+                  "sum": float(np.asarray(s[0], dtype=np.float64).sum()), "err": g.jit_error()}))
+g.close()
+"""
+
+
+def test_scene_specialised_cache_file_damage_recovers(tmp_path):
+    """The on-disk code-object cache: a second process loads the first one's build; a damaged cache
+    file is dropped and rebuilt, never fatal. Each probe runs in a fresh child process so the
+    in-process module cache does not hide the disk."""
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ, RTCORE_JIT_CACHE=str(tmp_path), RTCORE_JIT_FLAGS="-DRT_CACHE_TEST_SALT=1")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+    def probe():
+        r = subprocess.run([sys.executable, "-c", _CACHE_PROBE], env=env, cwd=root, capture_output=True,
+                           text=True, timeout=150)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return json.loads(r.stdout.strip().splitlines()[-1])
+
+    first = probe()
+    assert first["status"] == 1.0 and first["cached"] == 0.0, first
+    files = [f for f in os.listdir(tmp_path) if f.endswith(".co")]
+    assert len(files) == 1, files
+    second = probe()
+    assert second["status"] == 1.0 and second["cached"] == 1.0, second
+    with open(tmp_path / files[0], "wb") as f:
+        f.write(b"not a code object" * 64)
+    third = probe()
+    assert third["status"] == 1.0 and third["cached"] == 0.0, third
+    for r in (second, third):
+        assert r["rays"] == first["rays"] and r["sum"] == first["sum"]
+    assert os.path.getsize(tmp_path / files[0]) > 4096  # rewritten with the fresh build
