@@ -259,16 +259,24 @@ def main() -> int:
         parallelism = f"sample-sharded x{world}, RCCL reduce per step"
 
     def run(first: int, count: int) -> list:
+        # each launch records its own hipEvent pair around the path kernel (a ring of 64 per scene):
+        # the steps queue without a host sync and their kernel times are read every 64 steps
         kernel_ms = []
         pending = None
+        queued = 0
         for k in range(first, first + count):
             step(k)
-            kernel_ms.append(gpu.last_kernel_ms())  # hipEvent pair around this step's path kernel
+            queued += 1
+            if queued == gpu.KERNEL_TIME_RING:
+                kernel_ms += gpu.kernel_times(queued)
+                queued = 0
             if pending is not None:
                 finish_merge(pending)
             pending = start_merge(k)
         if pending is not None:
             finish_merge(pending)
+        if queued:
+            kernel_ms += gpu.kernel_times(queued)
         return kernel_ms
 
     run(0, args.warmup)

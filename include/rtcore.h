@@ -38,8 +38,9 @@
 extern "C" {
 #endif
 
-#define RTCORE_ABI_VERSION 3 /* 2: rt_frame_*, rt_render_bands, sample_base in rt_render_frame_multi;
-                                3: rt_set_jit, rt_scene_get_jit_error, build stats [15..17] */
+#define RTCORE_ABI_VERSION 4 /* 2: rt_frame_*, rt_render_bands, sample_base in rt_render_frame_multi;
+                                3: rt_set_jit, rt_scene_get_jit_error, build stats [15..17];
+                                4: rt_kernel_times */
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -267,8 +268,15 @@ int rt_render_device(rt_scene* scene, int32_t x0, int32_t y0, int32_t w, int32_t
 int rt_primary_ids_device(rt_scene* scene, int32_t x0, int32_t y0, int32_t w, int32_t h,
                           int32_t* d_ids, void* stream);
 
-/* Duration in ms of the last path-tracing kernel launched on this scene (hipEvent pair). */
+/* Duration in ms of the last path-tracing kernel launched on this scene (hipEvent pair).
+ * Waits for that kernel.  RT_ERR_ARG before the first launch. */
 int rt_last_kernel_ms(rt_scene* scene, float* ms);
+
+/* Durations in ms of the last n path-tracing kernels launched on this scene, oldest first
+ * (1 <= n <= 64 and n <= the launches so far, else RT_ERR_ARG).  Each launch records its own
+ * event pair in a ring of 64, so a caller can queue up to 64 launches without a host sync and
+ * read their times afterwards.  Waits for those kernels. */
+int rt_kernel_times(rt_scene* scene, int32_t n, float* ms);
 
 /*
  * Instrumentation (profiling builds of the measurement, not the render): while enabled, the

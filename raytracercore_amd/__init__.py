@@ -23,7 +23,7 @@ LIB_PATH = os.path.join(_HERE, "librtcore_hip.so")
 REPO_ROOT = os.path.dirname(_HERE)
 
 RT_OK = 0
-ABI_VERSION = 3  # RTCORE_ABI_VERSION of include/rtcore.h
+ABI_VERSION = 4  # RTCORE_ABI_VERSION of include/rtcore.h
 RT_PRIM_TRIANGLE, RT_PRIM_SPHERE, RT_PRIM_PLANE = 0, 1, 2
 RT_FLAG_MIRROR, RT_FLAG_TWOSIDED, RT_FLAG_INVERT, RT_FLAG_HASNORMALS, RT_FLAG_TRANSFORMED = 1, 2, 4, 8, 16
 RT_CAMERA_FRUSTUM, RT_CAMERA_ORTHO = 0, 1
@@ -142,6 +142,7 @@ def load_library(path: str = "") -> C.CDLL:
                              [C.c_void_p] * 4 + [C.c_void_p]),
         "rt_primary_ids_device": (C.c_int, [C.c_void_p] + [C.c_int32] * 4 + [C.c_void_p, C.c_void_p]),
         "rt_last_kernel_ms": (C.c_int, [C.c_void_p, P(C.c_float)]),
+        "rt_kernel_times": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_float)]),
         "rt_scene_set_stats": (C.c_int, [C.c_void_p, C.c_int32]),
         "rt_scene_get_stats": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_int32]),
         "rt_render_frame_multi": (C.c_int, [P(rt_scene_params), P(rt_prim), C.c_int32, P(rt_camera), C.c_int32,
@@ -389,6 +390,15 @@ class GpuRaytracer:
         ms = C.c_float(0)
         _check(self.lib.rt_last_kernel_ms(self.handle, C.byref(ms)))
         return float(ms.value)
+
+    KERNEL_TIME_RING = 64
+
+    def kernel_times(self, n: int) -> List[float]:
+        """rt_kernel_times: durations (ms) of the last n path kernels on this scene, oldest first
+        (n <= 64): launches queued without a host sync, timed afterwards."""
+        out = (C.c_float * max(n, 1))()
+        _check(self.lib.rt_kernel_times(self.handle, n, out))
+        return [float(v) for v in out[:n]]
 
     STAT_NAMES = ("node_visits", "tri_tests", "sph_tests", "cyc_start", "cyc_trace", "cyc_shade", "wave_iters",
                   "max_query_steps")

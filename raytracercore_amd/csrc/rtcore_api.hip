@@ -183,7 +183,11 @@ struct rt_scene {
     unsigned params_next = 0;
     bool has_camera = false;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // Timing of the path kernels: the i-th launch records the event pair i % kTimeRing, so a caller
+    // can queue up to that many launches before it reads their durations (rt_kernel_times).
+    static constexpr int kTimeRing = 64;
+    std::array<hipEvent_t, kTimeRing> t_start{}, t_end{};
+    uint64_t launches = 0;
     // Launches share per-scene scratch (partials, work counter, stack overflow area).  The end of
     // the last render operation is recorded here; an operation on a different stream waits for it.
     hipEvent_t done_ev = nullptr;
@@ -197,8 +201,10 @@ struct rt_scene {
         for (hipEvent_t e : slot_ev)
             if (e) (void)hipEventDestroy(e);
         if (done_ev) (void)hipEventDestroy(done_ev);
-        if (ev0) (void)hipEventDestroy(ev0);
-        if (ev1) (void)hipEventDestroy(ev1);
+        for (int i = 0; i < kTimeRing; i++) {
+            if (t_start[i]) (void)hipEventDestroy(t_start[i]);
+            if (t_end[i]) (void)hipEventDestroy(t_end[i]);
+        }
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -1108,7 +1114,7 @@ int resolve_traversal(rt_scene* s)
 }
 
 PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint64_t seed, uint64_t base);
-int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t stream);
+int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t stream, bool timed = true);
 int prepare_jit(rt_scene* s);
 int end_op(rt_scene* s, hipStream_t stream);
 
@@ -1141,7 +1147,7 @@ int calibrate_grouping(rt_scene* s)
     s->stats_blocks_per_cu = s->blocks_per_cu;
     PathParams p = make_params(s, x0, y0, w, h, 2, 0x5EEDull, 0);
     p.pool = 64; // one chunk per pool: the counts must not depend on the pool size
-    int rc = run_path(s, p, s->rays.p, s->stream);
+    int rc = run_path(s, p, s->rays.p, s->stream, false); // an internal probe: not in rt_kernel_times
     if (rc == RT_OK) rc = end_op(s, s->stream);
     s->stats_on = was_on;
     s->stats_blocks_per_cu = was_blocks;
@@ -1300,7 +1306,7 @@ int prepare_jit(rt_scene* s)
 }
 
 // Launch the path kernel for p (work buffers sized here), timing it with the scene's events.
-int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t stream)
+int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t stream, bool timed)
 {
     const size_t need = (size_t)p.n_chunks * (size_t)p.n_pad;
     if (need > 0xF0000000ull) { // 32-bit work-item counter (plus the pools' overshoot)
@@ -1324,7 +1330,8 @@ int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t
     }
     const int jit = prepare_jit(s);
     const int jit_grid = jit ? s->n_cu * s->jit.blocks_per_cu : 0;
-    HIP_TRY(hipEventRecord(s->ev0, stream));
+    const int tslot = (int)(s->launches % rt_scene::kTimeRing);
+    if (timed) HIP_TRY(hipEventRecord(s->t_start[tslot], stream));
     if (!s->params_h) {
         HIP_TRY(hipHostMalloc(&s->params_h, sizeof(PathParams) * rt_scene::kParamRing, hipHostMallocDefault));
         HIP_TRY(s->params_d.reserve(rt_scene::kParamRing));
@@ -1346,7 +1353,10 @@ int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t
     } else {
         HIP_TRY(launch_path(s->dev, s->camf_d.p, s->params_d.p + slot, s->variant, grid, stream, s->stats_on));
     }
-    HIP_TRY(hipEventRecord(s->ev1, stream));
+    if (timed) {
+        HIP_TRY(hipEventRecord(s->t_end[tslot], stream));
+        s->launches++;
+    }
     return RT_OK;
 }
 
@@ -1786,8 +1796,10 @@ int rt_scene_create(const rt_scene_params* params, const rt_prim* prims, int32_t
     HIP_TRY(hipGetDeviceProperties(&prop, device));
     s->n_cu = prop.multiProcessorCount;
     HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreate(&s->ev0));
-    HIP_TRY(hipEventCreate(&s->ev1));
+    for (int i = 0; i < rt_scene::kTimeRing; i++) {
+        HIP_TRY(hipEventCreate(&s->t_start[i]));
+        HIP_TRY(hipEventCreate(&s->t_end[i]));
+    }
     HIP_TRY(hipEventCreateWithFlags(&s->done_ev, hipEventDisableTiming));
     using clk = std::chrono::steady_clock;
     auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
@@ -1904,16 +1916,33 @@ int rt_render_device(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, 
     return end_op(s, st);
 }
 
+int rt_kernel_times(rt_scene* s, int32_t n, float* ms)
+{
+    if (!s || !ms || n < 1 || n > rt_scene::kTimeRing || (uint64_t)n > s->launches) {
+        set_error("rt_kernel_times: bad argument (n must be 1.." + std::to_string(rt_scene::kTimeRing) +
+                  " and at most the launches so far)");
+        return RT_ERR_ARG;
+    }
+    HIP_TRY(hipSetDevice(s->device));
+    for (int i = 0; i < n; i++) { // oldest first
+        const int slot = (int)((s->launches - (uint64_t)n + (uint64_t)i) % rt_scene::kTimeRing);
+        HIP_TRY(hipEventSynchronize(s->t_end[slot]));
+        HIP_TRY(hipEventElapsedTime(ms + i, s->t_start[slot], s->t_end[slot]));
+    }
+    return RT_OK;
+}
+
 int rt_last_kernel_ms(rt_scene* s, float* ms)
 {
     if (!s || !ms) {
         set_error("rt_last_kernel_ms: bad argument");
         return RT_ERR_ARG;
     }
-    HIP_TRY(hipSetDevice(s->device));
-    HIP_TRY(hipEventSynchronize(s->ev1));
-    HIP_TRY(hipEventElapsedTime(ms, s->ev0, s->ev1));
-    return RT_OK;
+    if (s->launches == 0) {
+        set_error("rt_last_kernel_ms: no path kernel launched on this scene yet");
+        return RT_ERR_ARG;
+    }
+    return rt_kernel_times(s, 1, ms);
 }
 
 int rt_scene_set_stats(rt_scene* s, int32_t enable)

@@ -350,6 +350,40 @@ def test_many_launches_two_streams(rc, scenes):
     assert np.allclose(s, s2, rtol=1e-5, atol=1e-5)
 
 
+def test_kernel_times_ring(rc, scenes):
+    """rt_kernel_times: launches queued without a host sync keep their own event pairs (a ring of
+    64); the last entry is rt_last_kernel_ms, a longer launch times longer, bad counts fail."""
+    import torch
+
+    scene = scenes["bounce.txt"]
+    W, H = 256, 192
+    gpu = rc.GpuRaytracer(scene, 0, size=(W, H))
+    with pytest.raises(rc.RtError):
+        gpu.last_kernel_ms()  # nothing launched yet
+    dev = torch.device("cuda", 0)
+    d_sum = torch.zeros(3 * W * H, dtype=torch.float64, device=dev)
+    d_n = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    d_m = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    d_r = torch.zeros(1, dtype=torch.int64, device=dev)
+    spps = [1, 256, 1, 256] * 17  # 68 launches: the ring wraps
+    for k, spp in enumerate(spps):
+        gpu.render_device(0, 0, W, H, spp, 2, 100 * k, d_sum.data_ptr(), d_n.data_ptr(), d_m.data_ptr(),
+                          d_r.data_ptr(), 0)
+    t = gpu.kernel_times(64)
+    assert len(t) == 64 and all(v > 0 for v in t)
+    assert t[-1] == gpu.last_kernel_ms()
+    # the ring holds the last 64 launches, oldest first: launches 4..67, spp 1, 256, 1, 256, ...
+    assert min(t[1::2]) > 1.5 * max(t[0::2])
+    for bad in (0, 65):
+        with pytest.raises(rc.RtError):
+            gpu.kernel_times(bad)
+    g2 = rc.GpuRaytracer(scene, 0, size=(W, H))
+    g2.render_tile(0, 0, 8, 8, 1)
+    assert len(g2.kernel_times(1)) == 1
+    with pytest.raises(rc.RtError):
+        g2.kernel_times(2)  # only one launch so far
+
+
 def test_errors_fail_loudly(rc, scenes):
     scene = scenes["bounce.txt"]
     gpu = rc.GpuRaytracer(scene, 0, size=(64, 64))
