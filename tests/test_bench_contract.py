@@ -1,0 +1,51 @@
+"""bench.py's output contract on the GPU: one JSON line with the driver's keys, the roofline and
+the CPU baseline, at N = 1 and on the N > 1 path (two ranks on one device over gloo, the rehearsal
+mode; RCCL refuses two ranks on one GPU).  Small spp keeps each run to seconds."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"}
+
+
+def _last_json(out: str) -> dict:
+    lines = [l for l in out.strip().splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out[-2000:]  # rank 0 prints exactly one line
+    return json.loads(lines[0])
+
+
+def test_bench_line_single_gpu():
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--spp", "16"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["higher_is_better"] is True
+    assert d["scaling"] == "weak" and d["vs_baseline"] is None and d["value"] > 0 and d["ms_per_step"] > 0
+    assert d["config"]["workload"].startswith("bounce.txt")
+    rf = d["roofline"]
+    assert {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(rf)
+    assert 0 < rf["frac"] < 1 and rf["achieved"] == pytest.approx(rf["frac"] * rf["peak"], rel=1e-2)
+    cb = d["cpu_baseline"]
+    assert {"value", "unit", "cores", "kind", "sample"} <= set(cb) and cb["value"] > 0 and cb["kind"] == "port"
+    # value: rays over the timed wall clock; kernel time is within it
+    assert d["kernel_ms"] <= d["ms_per_step"] * 1.001
+
+
+def test_bench_two_ranks_one_device():
+    env = dict(os.environ, RTCORE_BENCH_SAME_DEVICE="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", "29561", "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--spp", "8", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert "x2" in d["config"]["parallelism"]
