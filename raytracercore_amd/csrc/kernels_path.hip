@@ -254,7 +254,7 @@ __device__ __forceinline__ bool slab(float4 lo, float4 hi, V3 oi, V3 id, float t
 template <bool CULL, bool STATS, class SceneT, class GroupP, class TestP, class RectP, class FrameP, class BoxP, class XfP>
 __device__ __forceinline__ void trace_brute(const SceneT& s, GroupP groups, TestP tests, RectP rects, FrameP frames,
                                             BoxP boxes, XfP xf, V3 o, V3 d, int prev, Best& b, unsigned& n_flat,
-                                            unsigned& n_sph)
+                                            unsigned& n_sph, unsigned& n_node)
 {
     const V3 id = v3(slab_rcp(d.x), slab_rcp(d.y), slab_rcp(d.z));
     const V3 oi = o * id;
@@ -265,6 +265,7 @@ __device__ __forceinline__ void trace_brute(const SceneT& s, GroupP groups, Test
     for (int g = 0; g < n_groups; g++) {
         const GroupRec G = groups[g];
         if (CULL) {
+            if (STATS) n_node++; // the group's box: a node of a one-level tree (SURVEY 8(d) N_node)
             float tn;
             if (!__any(slab(G.lo, G.hi, oi, id, b.t, tn))) continue;
         }
@@ -972,15 +973,15 @@ __device__ __forceinline__ void path_body(const CameraF* __restrict__ camp, cons
 #ifdef RT_EXP_DUP_TRACE // cost experiment: a second closest-hit query from a perturbed origin
             {
                 Best b2{__builtin_huge_valf(), -1};
-                unsigned u0 = 0, u1 = 0;
+                unsigned u0 = 0, u1 = 0, u2 = 0;
                 trace_brute<CULL, false>(sc, groups, tests, rects, frames, boxes, xf,
-                                         S.o + v3(exp_sink * 1e-30f, 0, 0), S.d, S.prev, b2, u0, u1);
+                                         S.o + v3(exp_sink * 1e-30f, 0, 0), S.d, S.prev, b2, u0, u1, u2);
                 exp_sink += b2.t;
             }
 #endif
 #ifndef RT_EXP_NO_TRACE // cost experiment: every camera ray misses (per-sample overhead alone)
             trace_brute<CULL, STATS>(sc, groups, tests, rects, frames, boxes, xf, S.o, S.d, S.prev, b, cnt.tris,
-                                     cnt.sphs);
+                                     cnt.sphs, cnt.nodes);
 #endif
             const int pln0 = sc.n_bvh;
             for (int i = pln0; i < pln0 + sc.n_pln; i++) {
