@@ -149,6 +149,42 @@ def test_full_1080p_properties(rc, scenes):
     assert (full_miss == (ids < 0)).mean() > 0.99
 
 
+@pytest.mark.parametrize("config", ["die1080", "die4k", "mesh1080"])
+def test_bench_configs_full_size_properties(rc, scenes, config):
+    """The other bench workloads at their full sizes (C3 die 1080p x 1024 spp, C5 die 4K x 512 spp
+    per GPU, C4 the 1 M-triangle mesh 1080p x 64 spp), through size-independent properties:
+    every pixel gets exactly spp samples, radiance is finite and non-negative, the launch is
+    bit-reproducible, and the ray count lies within [samples, samples x (Recursion + 1)]."""
+    import torch
+
+    if config == "mesh1080":
+        from raytracercore_amd.scenes import mesh_scene_text
+
+        scene, (W, H, spp) = rc.SceneLoader.from_text(mesh_scene_text()), (1920, 1080, 64)
+    else:
+        scene = scenes["die.txt"]
+        W, H, spp = (1920, 1080, 1024) if config == "die1080" else (3840, 2160, 512)
+    gpu = rc.GpuRaytracer(scene, 0, size=(W, H))
+    dev = torch.device("cuda", 0)
+    outs = []
+    for _ in range(2):
+        d_sum = torch.zeros(3 * W * H, dtype=torch.float64, device=dev)
+        d_n = torch.zeros(W * H, dtype=torch.int32, device=dev)
+        d_m = torch.zeros(W * H, dtype=torch.int32, device=dev)
+        d_r = torch.zeros(1, dtype=torch.int64, device=dev)
+        gpu.render_device(0, 0, W, H, spp, 0, 0, d_sum.data_ptr(), d_n.data_ptr(), d_m.data_ptr(), d_r.data_ptr(),
+                          torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        ok = bool(torch.all(d_n + d_m == spp).item()) and bool(torch.all(torch.isfinite(d_sum)).item())
+        outs.append((ok, bool(torch.all(d_sum >= 0).item()), d_sum, d_n, int(d_r.item())))
+    (ok0, nn0, s0, n0, r0), (ok1, _, s1, n1, r1) = outs
+    assert ok0 and ok1 and nn0
+    assert torch.equal(s0, s1) and torch.equal(n0, n1) and r0 == r1, "not bit-reproducible"
+    samples = W * H * spp
+    assert samples <= r0 <= samples * (scene.params.recursion + 1)
+    gpu.close()
+
+
 def test_sample_ranges_compose(rc, scenes):
     """Rendering samples [0, a) and [a, a+b) accumulates the same samples as [0, a+b)."""
     scene = scenes["die.txt"]
