@@ -6,6 +6,7 @@
 // could reach is still reached.  Nodes store both children's boxes (64 B per visit, one
 // cache line) and child references encode leaves inline (rt_internal.h NodeF).
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 
@@ -55,6 +56,7 @@ struct BNode {
     FBox box;
     int left = -1, right = -1;
     int first = 0, count = 0;
+    bool cut = false; // a leaf of the BVH2 (count <= max_leaf); with `full` its subtree is built on
 };
 
 struct Ref {
@@ -67,12 +69,15 @@ struct SahBuilder {
     std::vector<Ref> refs;
     std::vector<BNode> nodes;
     int max_leaf;
+    bool full = false; // build on below the BVH2 leaves down to single primitives (for the wide collapse)
     int max_depth = 0;
 
-    int build(int first, int count, int depth)
+    int build(int first, int count, int depth, bool below = false)
     {
-        max_depth = std::max(max_depth, depth);
+        if (!below) max_depth = std::max(max_depth, depth);
         BNode n;
+        n.first = first;
+        n.count = count;
         n.box.empty();
         FBox cb;
         cb.empty();
@@ -84,12 +89,10 @@ struct SahBuilder {
             }
         }
         int me = (int)nodes.size();
+        const bool cut = count <= max_leaf;
+        n.cut = cut;
         nodes.push_back(n);
-        if (count <= max_leaf && count <= 8) {
-            nodes[me].first = first;
-            nodes[me].count = count;
-            return me;
-        }
+        if (cut && (!full || count == 1)) return me;
         // binned SAH over the centroid bounds
         const int B = 32;
         int best_axis = -1, best_split = -1;
@@ -134,15 +137,8 @@ struct SahBuilder {
                 }
             }
         }
-        float leaf_cost = n.box.area() * count;
-        float split_cost = 0.125f * n.box.area() + best_cost; // traversal step ~1/8 of a primitive test
         int mid;
-        if (best_axis < 0 || (count <= max_leaf && split_cost >= leaf_cost)) {
-            if (count <= max_leaf) {
-                nodes[me].first = first;
-                nodes[me].count = count;
-                return me;
-            }
+        if (best_axis < 0) {
             // all centroids coincide (or no useful split): median split by index
             mid = first + count / 2;
         } else {
@@ -155,8 +151,8 @@ struct SahBuilder {
             mid = (int)(it - refs.begin());
             if (mid == first || mid == first + count) mid = first + count / 2;
         }
-        int l = build(first, mid - first, depth + 1);
-        int r = build(mid, first + count - mid, depth + 1);
+        int l = build(first, mid - first, depth + 1, below || cut);
+        int r = build(mid, first + count - mid, depth + 1, below || cut);
         nodes[me].left = l;
         nodes[me].right = r;
         return me;
@@ -178,11 +174,12 @@ void sah_prim_box(const HostPrim& p, float lo[3], float hi[3])
     }
 }
 
-SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf)
+SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf, bool full)
 {
     SahBvh out;
     SahBuilder b;
     b.max_leaf = std::max(1, std::min(8, max_leaf));
+    b.full = full;
     for (int i = 0; i < (int)prims.size(); i++) {
         const HostPrim& p = prims[i];
         if (p.kind == RT_PRIM_PLANE) continue;
@@ -207,7 +204,7 @@ SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf)
     while (!stack.empty()) {
         int i = stack.back();
         stack.pop_back();
-        if (b.nodes[i].left < 0) continue;
+        if (b.nodes[i].left < 0 || b.nodes[i].cut) continue;
         remap[i] = (int)internal.size();
         internal.push_back(i);
         stack.push_back(b.nodes[i].right);
@@ -215,7 +212,7 @@ SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf)
     }
     auto ref_of = [&](int i) {
         const BNode& n = b.nodes[i];
-        return n.left < 0 ? leaf_ref(n.first, n.count) : remap[i];
+        return (n.left < 0 || n.cut) ? leaf_ref(n.first, n.count) : remap[i];
     };
     out.root = ref_of(root);
     for (int i : internal) {
@@ -232,6 +229,22 @@ SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf)
         f.rmin = make_float4(r.box.lo[0], r.box.lo[1], r.box.lo[2], rw);
         f.rmax = make_float4(r.box.hi[0], r.box.hi[1], r.box.hi[2], 0.0f);
         out.nodes.push_back(f);
+    }
+    if (full) { // the whole tree down to single primitives, pre-order (children after their parent)
+        out.full.resize(b.nodes.size());
+        for (size_t i = 0; i < b.nodes.size(); i++) {
+            const BNode& n = b.nodes[i];
+            SahFullNode& f = out.full[i];
+            for (int k = 0; k < 3; k++) {
+                f.lo[k] = n.box.lo[k];
+                f.hi[k] = n.box.hi[k];
+            }
+            f.left = n.left;
+            f.right = n.right;
+            f.first = n.first;
+            f.count = n.count;
+        }
+        out.full_root = root;
     }
     return out;
 }
@@ -312,11 +325,129 @@ struct W4Builder {
     }
 };
 
+// SAH-optimal collapse of the whole tree.  C[i][j] is the least cost of node i's subtree when it
+// may fill up to j child slots of its parent wide node: one slot (i itself as a leaf or as a wide
+// node) or i opened and its slots shared by its two children.
+struct W4Sah {
+    const std::vector<SahFullNode>& t;
+    WideCosts w;
+    std::vector<std::array<float, 5>> C;
+    std::vector<std::array<int8_t, 5>> use;   // use[i][j]: slots actually taken (1 = i itself)
+    std::vector<std::array<int8_t, 5>> split; // split[i][j]: slots of the left child when opened with j
+    std::vector<uint8_t> leaf;                // i itself (one slot) is a leaf, not a wide node
+    std::vector<Node4Q> out;
+    int stack_need = 0;
+    int depth = 0;
+
+    static float area(const SahFullNode& n)
+    {
+        float d[3];
+        for (int k = 0; k < 3; k++) d[k] = std::max(0.0f, n.hi[k] - n.lo[k]);
+        return 2.0f * (d[0] * d[1] + d[1] * d[2] + d[2] * d[0]);
+    }
+    void solve()
+    {
+        const int n = (int)t.size();
+        C.resize(n);
+        use.resize(n);
+        split.resize(n);
+        leaf.resize(n);
+        for (int i = n - 1; i >= 0; i--) { // children come after their parent (pre-order)
+            const SahFullNode& s = t[i];
+            const float a = area(s);
+            if (s.left < 0) {
+                for (int j = 1; j <= 4; j++) {
+                    C[i][j] = w.c_prim * a * (float)s.count;
+                    use[i][j] = 1;
+                }
+                leaf[i] = 1;
+                continue;
+            }
+            float dist[5];
+            for (int j = 2; j <= 4; j++) {
+                dist[j] = __builtin_huge_valf();
+                for (int k = 1; k < j; k++) {
+                    const float c = C[s.left][k] + C[s.right][j - k];
+                    if (c < dist[j]) {
+                        dist[j] = c;
+                        split[i][j] = (int8_t)k;
+                    }
+                }
+            }
+            const float c_node = w.c_node * a + dist[4];
+            const float c_leaf = s.count <= w.max_leaf ? w.c_prim * a * (float)s.count : __builtin_huge_valf();
+            leaf[i] = c_leaf <= c_node;
+            C[i][1] = leaf[i] ? c_leaf : c_node;
+            use[i][1] = 1;
+            for (int j = 2; j <= 4; j++) {
+                if (dist[j] < C[i][j - 1]) {
+                    C[i][j] = dist[j];
+                    use[i][j] = (int8_t)j;
+                } else {
+                    C[i][j] = C[i][j - 1];
+                    use[i][j] = use[i][j - 1];
+                }
+            }
+        }
+    }
+    void expand(int i, int j, std::vector<int>& ch) const
+    {
+        const int u = use[i][j];
+        if (u == 1) {
+            ch.push_back(i);
+            return;
+        }
+        expand(t[i].left, split[i][u], ch);
+        expand(t[i].right, u - split[i][u], ch);
+    }
+    int ref_of_leaf(int i) const { return leaf_ref(t[i].first, t[i].count); }
+    // the wide node of tree node i (pre-order, as the greedy collapse); returns its index
+    int emit(int i, int level, int pushes)
+    {
+        depth = std::max(depth, level);
+        std::vector<int> ch;
+        expand(t[i].left, split[i][4], ch);
+        expand(t[i].right, 4 - split[i][4], ch);
+        const int me = (int)out.size();
+        out.push_back(Node4Q{});
+        const int nc = (int)ch.size();
+        stack_need = std::max(stack_need, pushes + nc - 1);
+        int refs[4] = {RT_NODE4_EMPTY, RT_NODE4_EMPTY, RT_NODE4_EMPTY, RT_NODE4_EMPTY};
+        float lo[4][3], hi[4][3];
+        for (int k = 0; k < nc; k++) {
+            const int c = ch[k];
+            refs[k] = leaf[c] ? ref_of_leaf(c) : emit(c, level + 1, pushes + nc - 1);
+            for (int a = 0; a < 3; a++) {
+                lo[k][a] = t[c].lo[a];
+                hi[k][a] = t[c].hi[a];
+            }
+        }
+        out[me] = quantize_node4(lo, hi, refs, nc);
+        return me;
+    }
+};
+
 } // namespace
 
-Bvh4 build_bvh4(const SahBvh& b2)
+Bvh4 build_bvh4(const SahBvh& b2, const WideCosts* sah)
 {
     Bvh4 r;
+    if (sah && !b2.full.empty()) {
+        W4Sah w{b2.full, *sah, {}, {}, {}, {}, {}, 0, 0};
+        w.w.max_leaf = std::max(1, std::min(8, w.w.max_leaf));
+        w.solve();
+        const int root = b2.full_root;
+        if (w.leaf[root]) {
+            r.root = w.ref_of_leaf(root);
+            return r;
+        }
+        w.out.reserve(b2.full.size() / 4 + 1);
+        r.root = w.emit(root, 0, 0);
+        r.nodes = std::move(w.out);
+        r.stack_need = w.stack_need;
+        r.depth = w.depth;
+        return r;
+    }
     if (b2.nodes.empty()) { // a single leaf (or nothing)
         r.root = b2.root;
         return r;

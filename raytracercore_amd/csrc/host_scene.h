@@ -69,14 +69,24 @@ struct RefBvh {
 };
 RefBvh build_ref_bvh(const std::vector<HostPrim>& prims);
 
+// One node of the whole binned-SAH tree (down to single primitives): the input of the SAH-optimal
+// wide collapse.  Primitives [first, first + count) of SahBvh::order lie below it.
+struct SahFullNode {
+    float lo[3], hi[3];
+    int left, right; // node indices, -1 for a single-primitive leaf
+    int first, count;
+};
+
 // Binned-SAH BVH2 for the fp32 path kernel (planes are excluded and tested separately).
 struct SahBvh {
     std::vector<NodeF> nodes;
     std::vector<int> order; // primitive IDs in leaf order
     int root = 0;           // child reference of the root
     int depth = 0;
+    std::vector<SahFullNode> full; // with build_sah_bvh(..., full = true): the tree below the leaves too
+    int full_root = 0;
 };
-SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf);
+SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf, bool full = false);
 // fp32 box of a primitive for the fast-path BVHs: the fp64 bounds padded by 2^-20 relative and
 // rounded outward (used by the host and the GPU builder alike)
 void sah_prim_box(const HostPrim& p, float lo[3], float hi[3]);
@@ -87,7 +97,16 @@ struct Bvh4 {
     int stack_need = 0; // deepest traversal stack any ray can need
     int depth = 0;
 };
-Bvh4 build_bvh4(const SahBvh& bvh2);
+// Wide collapse.  Greedy (no costs given, or no full tree): each wide node opens its largest-area
+// internal child until it has four children, over the BVH2's own leaves.  SAH-optimal (costs
+// given and SahBvh::full built): a dynamic program over the whole tree chooses the wide nodes and
+// the leaves (of at most max_leaf primitives) with the least surface-area cost, c_node per wide-node
+// visit and c_prim per primitive test (after Ylitie, Karras and Laine 2017, for 4-wide nodes).
+struct WideCosts {
+    float c_node = 1.0f, c_prim = 0.5f;
+    int max_leaf = 3;
+};
+Bvh4 build_bvh4(const SahBvh& bvh2, const WideCosts* sah = nullptr);
 
 // Camera.InitRender restated for both precisions.
 void camera_init(const rt_camera& cam, int width, int height, CameraD& d, CameraF& f);

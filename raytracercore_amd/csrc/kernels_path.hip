@@ -777,7 +777,13 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
                 const unsigned q = L.item & 63u, t = L.item >> 6;
                 const int c = (int)(t & (unsigned)(p.n_chunks - 1));
                 unsigned by, bx;
-                divmod(t >> p.log2_chunks, (unsigned)p.blocks_x, p.inv_blocks_x, by, bx);
+                const unsigned blk = t >> p.log2_chunks;
+                if (p.magic_bx != 0) { // multiply-high division (exact here, make_params checks)
+                    by = __umulhi(blk, p.magic_bx);
+                    bx = blk - by * (unsigned)p.blocks_x;
+                } else {
+                    divmod(blk, (unsigned)p.blocks_x, p.inv_blocks_x, by, bx);
+                }
                 const int px = (int)bx * 8 + (q & 7), py = (int)by * 8 + (q >> 3);
                 if (px < p.w && py < p.h && c * p.chunk < p.spp) {
                     L.item_open = true;

@@ -22,7 +22,9 @@ struct PathParams {
     int spec;                   // BVH kernel (RT_BVH_SPEC): lanes blocked on a pending leaf that trigger a leaf step
     int pool;                   // work items a wave takes per atomic: 64 x a power of two <= n_chunks
                                 // (all from one 8x8 block, so a wave's lanes stay on neighbouring pixels)
-    float inv_blocks_x;         // fp32 reciprocal for the item decode
+    float inv_blocks_x;         // fp32 reciprocal for the item decode (when magic_bx == 0)
+    unsigned magic_bx;          // ceil(2^32 / blocks_x) when block / blocks_x = umulhi(block, magic_bx) for
+                                // every block of the launch (make_params checks), else 0
     unsigned long long seed;
     rt_key2 seed_key;           // rt_rng_seed_key(seed) (rtcore_rng.h)
     unsigned long long sample_base;

@@ -1193,6 +1193,15 @@ PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint6
     p.blocks_x = (w + 7) / 8;
     p.n_pad = p.blocks_x * ((h + 7) / 8) * 64;
     p.inv_blocks_x = 1.0f / (float)p.blocks_x;
+    // Item decode by multiply-high (one v_mul_hi_u32) instead of the fp32-reciprocal divmod: exact
+    // for every block index x when x * (M * blocks_x - 2^32) < 2^32, M = ceil(2^32 / blocks_x).
+    p.magic_bx = 0;
+    if (p.blocks_x > 1 && !getenv("RTCORE_NO_MAGIC_DIV")) { // (the env variable: A/B of the decode)
+        const uint64_t M = ((1ull << 32) + (uint64_t)p.blocks_x - 1) / (uint64_t)p.blocks_x;
+        const uint64_t err = M * (uint64_t)p.blocks_x - (1ull << 32);
+        const uint64_t max_blk = (uint64_t)(p.n_pad / 64);
+        if (M < (1ull << 32) && max_blk * err < (1ull << 32)) p.magic_bx = (unsigned)M;
+    }
     // One device-scope atomic hands a wave p.pool items.  64 per atomic made the dispenser a
     // bottleneck (measured, 1080p: die.txt grouped 50.9 -> 47.0 ms with 256, 48.2 with 128 or 512;
     // bounce.txt flat 33.4 -> 33.0 ms with 128, 33.6 with 256; mesh BVH 82.2 -> 80.3 with 256).
@@ -1404,8 +1413,18 @@ int build_bvhs(rt_scene* s)
     if (const char* e = getenv("RTCORE_MAX_LEAF")) max_leaf = std::max(1, std::min(8, atoi(e))); // tuning
     s->bvh.builder = builder_for(nb);
     if (s->bvh.builder == RT_BVH_BUILDER_HOST) {
-        s->sah = build_sah_bvh(H, max_leaf);
-        s->bvh4 = build_bvh4(s->sah);
+        // the wide tree: greedy collapse of the BVH2 (default), or the SAH-optimal collapse of the
+        // whole SAH tree (RTCORE_WIDE_COLLAPSE=1; RTCORE_WIDE_CNODE / _CPRIM / _LEAF set its costs)
+        WideCosts wc;
+        bool sah_collapse = false; // measured slower on C4
+        if (const char* e = getenv("RTCORE_WIDE_COLLAPSE")) sah_collapse = atoi(e) != 0;
+        if (const char* e = getenv("RTCORE_WIDE_CNODE")) wc.c_node = (float)atof(e);
+        if (const char* e = getenv("RTCORE_WIDE_CPRIM")) wc.c_prim = (float)atof(e);
+        if (const char* e = getenv("RTCORE_WIDE_LEAF")) wc.max_leaf = std::max(1, std::min(8, atoi(e)));
+        s->sah = build_sah_bvh(H, max_leaf, sah_collapse);
+        s->bvh4 = build_bvh4(s->sah, sah_collapse ? &wc : nullptr);
+        s->sah.full.clear(); // only the collapse reads the whole tree
+        s->sah.full.shrink_to_fit();
         s->bvh.n_nodes2 = (int)s->sah.nodes.size();
         s->bvh.root2 = s->sah.root;
         s->bvh.depth2 = s->sah.depth;

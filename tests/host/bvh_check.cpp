@@ -1,12 +1,12 @@
 // bvh_check.cpp -- host-side structural checks of the fast-path acceleration structures
 // (built by tests/test_host.py through `make -C raytracercore_amd/csrc bvh_check`).
 //
-// For a scene file: the binned-SAH BVH2 and its 4-wide quantised collapse must
+// For a scene file: the binned-SAH BVH2 and both 4-wide quantised collapses (greedy, SAH-optimal) must
 //   * reference every non-plane primitive exactly once;
 //   * have, for every wide node, dequantised child planes (origin + q * 2^e, in exact
 //     arithmetic) that contain every primitive box below that child;
 //   * never need more traversal-stack entries than the computed stack_need.
-// Prints "ok <n_prims> <bvh2 nodes> <wide nodes> <stack_need>" or the first failure.
+// Prints "ok <n_prims> <bvh2 nodes> <wide nodes> <stack_need>" per collapse or the first failure.
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -118,36 +118,41 @@ int main(int argc, char** argv)
     const auto t0 = clk::now();
     const std::vector<HostPrim> H = prepare_prims(ps.prims.data(), (int)ps.prims.size());
     const auto t1 = clk::now();
-    const SahBvh b2 = build_sah_bvh(H, H.size() > 256 ? 4 : 2);
+    const SahBvh b2 = build_sah_bvh(H, H.size() > 256 ? 4 : 2, true);
     const auto t2 = clk::now();
-    const Bvh4 b4 = build_bvh4(b2);
-    const auto t3 = clk::now();
-    if (std::getenv("BVH_CHECK_TIME")) {
-        auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
-        std::fprintf(stderr, "prepare %.1f ms, sah %.1f ms, collapse %.1f ms\n", ms(t1 - t0), ms(t2 - t1), ms(t3 - t2));
-    }
-    Ctx c;
-    c.H = &H;
-    c.b2 = &b2;
-    c.b4 = &b4;
-    c.seen.assign(H.size(), 0);
-    if (!b4.nodes.empty()) visit(c, b4.root, 0);
-    else if (b2.root < 0 && !b2.order.empty()) visit(c, b2.root, 0);
-    if (!c.ok) {
-        std::printf("FAIL %s\n", c.msg);
-        return 1;
-    }
-    for (size_t i = 0; i < H.size(); i++) {
-        const int want = H[i].kind == RT_PRIM_PLANE ? 0 : 1;
-        if (c.seen[i] != want) {
-            std::printf("FAIL prim %zu referenced %d times\n", i, c.seen[i]);
+    // both wide collapses: greedy over the BVH2's leaves, SAH-optimal over the whole tree
+    const WideCosts wc;
+    for (int mode = 0; mode < 2; mode++) {
+        const auto t3 = clk::now();
+        const Bvh4 b4 = build_bvh4(b2, mode ? &wc : nullptr);
+        const auto t4 = clk::now();
+        if (std::getenv("BVH_CHECK_TIME")) {
+            auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
+            std::fprintf(stderr, "prepare %.1f ms, sah %.1f ms, %s collapse %.1f ms\n", ms(t1 - t0), ms(t2 - t1),
+                         mode ? "sah" : "greedy", ms(t4 - t3));
+        }
+        Ctx c;
+        c.H = &H;
+        c.b2 = &b2;
+        c.b4 = &b4;
+        c.seen.assign(H.size(), 0);
+        if (!b4.nodes.empty() || (b4.root < 0 && !b2.order.empty())) visit(c, b4.root, 0);
+        if (!c.ok) {
+            std::printf("FAIL %s (%s collapse)\n", c.msg, mode ? "sah" : "greedy");
             return 1;
         }
+        for (size_t i = 0; i < H.size(); i++) {
+            const int want = H[i].kind == RT_PRIM_PLANE ? 0 : 1;
+            if (c.seen[i] != want) {
+                std::printf("FAIL prim %zu referenced %d times (%s collapse)\n", i, c.seen[i], mode ? "sah" : "greedy");
+                return 1;
+            }
+        }
+        if (c.max_stack > b4.stack_need) {
+            std::printf("FAIL stack %d > stack_need %d\n", c.max_stack, b4.stack_need);
+            return 1;
+        }
+        std::printf("%s %zu %zu %zu %d\n", mode ? "" : "ok", H.size(), b2.nodes.size(), b4.nodes.size(), b4.stack_need);
     }
-    if (c.max_stack > b4.stack_need) {
-        std::printf("FAIL stack %d > stack_need %d\n", c.max_stack, b4.stack_need);
-        return 1;
-    }
-    std::printf("ok %zu %zu %zu %d\n", H.size(), b2.nodes.size(), b4.nodes.size(), b4.stack_need);
     return 0;
 }
