@@ -3,6 +3,7 @@
 
 #include <hip/hiprtc.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -142,9 +143,34 @@ bool compile(const std::string& arch, const std::string& main_src, const std::st
 struct Entry {
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
+    int refs = 0;        // scenes holding fn (jit_kernel / jit_release)
+    uint64_t stamp = 0;  // last use, for the eviction of unreferenced modules
 };
 std::mutex g_mu;
-std::map<std::pair<int, uint64_t>, Entry> g_cache; // (device, key) -> loaded module (process lifetime)
+std::map<std::pair<int, uint64_t>, Entry> g_cache; // (device, key) -> loaded module
+uint64_t g_stamp = 0;
+
+// Unloads the least recently used unreferenced modules beyond kJitKeep (g_mu held).  A released
+// module may still run in launches queued before its release, so the device is synchronised first.
+void evict_unreferenced()
+{
+    std::vector<std::pair<uint64_t, std::pair<int, uint64_t>>> idle;
+    for (const auto& kv : g_cache)
+        if (kv.second.refs == 0 && kv.second.mod) idle.push_back({kv.second.stamp, kv.first});
+    if ((int)idle.size() <= kJitKeep) return;
+    std::sort(idle.begin(), idle.end());
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (size_t i = 0; i + kJitKeep < idle.size(); i++) {
+        const auto key = idle[i].second;
+        Entry& e = g_cache[key];
+        if (hipSetDevice(key.first) == hipSuccess && hipDeviceSynchronize() == hipSuccess) {
+            (void)hipModuleUnload(e.mod);
+            g_cache.erase(key);
+        }
+    }
+    (void)hipSetDevice(cur);
+}
 
 } // namespace
 
@@ -259,7 +285,20 @@ bool jit_kernel(int device, const std::string& header, bool grouped, JitKernel& 
         out.from_cache = true;
     }
     out.fn = e.fn;
+    e.refs++;
+    e.stamp = ++g_stamp;
+    evict_unreferenced(); // e is referenced, so it stays
     return true;
+}
+
+void jit_release(int device, hipFunction_t fn)
+{
+    std::lock_guard<std::mutex> lock(g_mu);
+    for (auto& kv : g_cache)
+        if (kv.first.first == device && kv.second.fn == fn && kv.second.refs > 0) {
+            kv.second.refs--;
+            return;
+        }
 }
 
 size_t jit_compile_check(const std::string& arch, bool grouped, std::string& err)

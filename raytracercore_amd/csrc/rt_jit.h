@@ -29,8 +29,13 @@ struct JitKernel {
 
 // The grouped (culling) or flat entry point built for `header` on `device` (the current device),
 // cached per process and on disk (RTCORE_JIT_CACHE, else $HOME/.cache/rtcore_jit, else /tmp).
-// Returns false with `err` set when hiprtc or the module load fails.
+// Returns false with `err` set when hiprtc or the module load fails.  A successful call holds a
+// reference on the module until jit_release; the process keeps at most kJitKeep modules nobody
+// references and unloads the least recently used beyond that (after synchronising its device), so
+// a caller that moves the camera often does not accumulate one loaded module per camera.
 bool jit_kernel(int device, const std::string& header, bool grouped, JitKernel& out, std::string& err);
+void jit_release(int device, hipFunction_t fn);
+constexpr int kJitKeep = 16;
 
 // Host only: compiles the embedded sources for `arch` with an empty scene; the code object size,
 // or 0 with `err` set (the CPU tests' check that the run-time build compiles).

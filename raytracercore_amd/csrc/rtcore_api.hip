@@ -197,6 +197,7 @@ struct rt_scene {
 
     ~rt_scene()
     {
+        if (jit.fn) jit_release(device, jit.fn); // (the stream is synchronised by rt_scene_destroy)
         if (params_h) (void)hipHostFree(params_h);
         for (hipEvent_t e : slot_ev)
             if (e) (void)hipEventDestroy(e);
@@ -1280,6 +1281,7 @@ int prepare_jit(rt_scene* s)
     s->jit.error.clear();
     s->jit.variant = s->variant;
     s->jit.gen = gen;
+    if (s->jit.fn) jit_release(s->device, s->jit.fn); // launches still queued keep it: eviction syncs the device
     s->jit.fn = nullptr;
     PathParams lp{};
     fill_launch(s->dev, s->variant, lp);

@@ -714,6 +714,27 @@ def test_scene_specialised_kernel_follows_camera_group_order(rc, scenes):
     assert not np.array_equal(a0[0], a2[0])
 
 
+def test_scene_specialised_many_cameras_evicts_and_matches(rc, scenes):
+    """One build per camera: after more camera changes than the process keeps unreferenced modules
+    (kJitKeep = 16), the least recently used are unloaded and the current build still renders
+    exactly what the generic kernel does."""
+    C_ = __import__("ctypes")
+    g = rc.GpuRaytracer(scenes["bounce.txt"], 0, size=(32, 24), traversal=rc.RT_TRAVERSAL_BRUTE)
+    cam = rc.rt_camera.from_buffer_copy(scenes["bounce.txt"].cameras[0])
+    for k in range(20):
+        cam.position.x += 0.01  # a new camera: a new specialised build, the previous one released
+        assert g.lib.rt_scene_set_camera(g.handle, C_.byref(cam)) == 0
+        a = g.render_tile(0, 0, 32, 24, 2, seed=k)
+        assert g.build_stats()["jit_status"] == 1.0
+    rc.set_jit(False)
+    try:
+        b = g.render_tile(0, 0, 32, 24, 2, seed=19)
+    finally:
+        rc.set_jit(True)
+    g.close()
+    assert a[3] == b[3] and np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
 def test_scene_specialised_build_failure_falls_back(rc, scenes, monkeypatch):
     """A failing run-time build (here: a bad compiler flag) leaves the generic kernel in charge:
     the render is unchanged, build statistic 15 reads -1 and rt_scene_get_jit_error says why."""
