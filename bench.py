@@ -228,7 +228,7 @@ def main() -> int:
                 sharding.scatter_slots(f_sum, f_n, f_m, got, rows, W, plane)
         expect_per_step = frame_spp
         parallelism = (f"row bands x{world} (interleaved {band}-row bands, {frame_spp} spp per frame), "
-                       f"RCCL gather per step")
+                       + ("RCCL gather per step" if world > 1 else "one GPU, no collective"))
     else:
         # sample sharding: every rank renders the whole frame with its own sample range; one RCCL
         # reduce per accumulator plane per step
@@ -256,7 +256,7 @@ def main() -> int:
                 f_n.add_(d_n)
                 f_m.add_(d_m)
         expect_per_step = spp * world
-        parallelism = f"sample-sharded x{world}, RCCL reduce per step"
+        parallelism = f"sample-sharded x{world}, " + ("RCCL reduce per step" if world > 1 else "one GPU, no collective")
 
     def run(first: int, count: int) -> list:
         # each launch records its own hipEvent pair around the path kernel (a ring of 64 per scene):
