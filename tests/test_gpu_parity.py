@@ -427,6 +427,14 @@ def test_errors_fail_loudly(rc, scenes):
         gpu.render_tile(60, 60, 8, 8, 1)  # outside the frame
     with pytest.raises(rc.RtError):
         gpu.primary_ids(0, 0, 0, 4)
+    with pytest.raises(rc.RtError):
+        gpu.render_tile(0, 0, 8, 8, -1)
+    s0, n0, m0, r0 = gpu.render_tile(0, 0, 8, 8, 0)  # zero samples: a no-op
+    assert not n0.any() and not m0.any() and not s0.any() and r0 == 0
+    with pytest.raises(rc.RtError):
+        gpu.render_tile(0, 0, 64, 64, 1 << 27)  # more work items than the 32-bit dispenser counts
+    s, n, m, rays = gpu.render_tile(0, 0, 8, 8, 2)  # the scene still renders after the refusals
+    assert (n + m == 2).all() and rays > 0
 
 
 def test_tonemap_device_matches_sample_output(rc, scenes):
