@@ -112,9 +112,17 @@ def path_stats(gpu, W, H, spp, seed, d_rays):
     gpu.set_stats(False)
     rays = max(1, int(d_rays.item()))
     cyc = st["cyc_start"] + st["cyc_trace"] + st["cyc_shade"]
-    return {"nodes": st["node_visits"] / rays, "tris": st["tri_tests"] / rays, "sphs": st["sph_tests"] / rays,
-            "cycles": {k: round(st["cyc_" + k] / max(1, cyc), 4) for k in ("start", "trace", "shade")},
-            "wave_iters_per_ray": round(st["wave_iters"] * 64 / rays, 4)}
+    out = {"nodes": st["node_visits"] / rays, "tris": st["tri_tests"] / rays, "sphs": st["sph_tests"] / rays,
+           "cycles": {k: round(st["cyc_" + k] / max(1, cyc), 4) for k in ("start", "trace", "shade")},
+           "wave_iters_per_ray": round(st["wave_iters"] * 64 / rays, 4)}
+    if gpu.info().traversal in (2, 3):  # BVH kernels: the three counters are lane slots, not cycles
+        slots = st["wave_iters"] * 64
+        node, leaf, idle, wait = st["node_visits"], st["cyc_start"], st["cyc_trace"], st["cyc_shade"]
+        out["cycles"] = None
+        out["lane_slots"] = {k: round(v / rays, 3) for k, v in (
+            ("node_step", node), ("leaf_step", leaf), ("traversing_idle", idle), ("waiting_for_shading", wait),
+            ("no_work", slots - node - leaf - idle - wait))}
+    return out
 
 
 def cpu_baseline(cfg_name: str, threads: int):
@@ -309,7 +317,9 @@ def main() -> int:
         my_rays_per_step = total_rays / (args.steps * world)  # the average rank's launch
         avg_ms = sum(kernel_ms) / len(kernel_ms)
         build = gpu.build_stats()  # of the timed launches (before the instrumented one below)
-        st = path_stats(gpu, W, H, max(1, spp // 16), args.seed, d_rays)
+        # the BVH kernels' lane-slot split depends on the launch's length (its tail), so they are
+        # instrumented at the timed launch's spp; the brute-force kernels at 1/16 of it
+        st = path_stats(gpu, W, H, spp if info.traversal in (2, 3) else max(1, spp // 16), args.seed, d_rays)
         fpr = flops_per_ray(st, scene)
         bpr = bytes_per_ray(st, scene)
         out = {
@@ -339,7 +349,7 @@ def main() -> int:
             "roofline": roofline(args.config, fpr, bpr, my_rays_per_step, avg_ms),
             "path_stats": {"per_ray": {k: round(st[k], 3) for k in ("nodes", "tris", "sphs")},
                            "lane_slots_per_ray": st["wave_iters_per_ray"],
-                           "wave_cycles": st["cycles"]},
+                           **({"wave_cycles": st["cycles"]} if st["cycles"] else {"lane_slots": st["lane_slots"]})},
             "scene_build": {"builder": ["auto", "host", "gpu"][info.bvh_builder],
                             **{k: round(v, 2) for k, v in build.items()}},
         }

@@ -1125,6 +1125,15 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
         const bool can_node = trav && more && ref >= 0;
         const bool blocked = trav && k < kend && !can_node;
         const bool leaf_step = __ballot(can_node) == 0 || __popcll(__ballot(blocked)) >= p.spec; // wave-uniform
+        if (STATS) { // lane slots of this iteration (the BVH kernels reuse the brute-force cycle counters):
+                     // testing a leaf | traversing but idle in this step's kind | waiting for the shading phase
+            const unsigned n_trav = (unsigned)__popcll(__ballot(trav));
+            const unsigned n_node = leaf_step ? 0u : (unsigned)__popcll(__ballot(can_node));
+            const unsigned n_leaf = leaf_step ? (unsigned)__popcll(__ballot(trav && k < kend)) : 0u;
+            cnt.cyc_start += n_leaf;
+            cnt.cyc_trace += n_trav - n_node - n_leaf;
+            cnt.cyc_shade += (unsigned)__popcll(__ballot(!trav && (L.active || L.live)));
+        }
         if (trav) {
             if (leaf_step) {
                 if (k < kend) { // RT_SPEC_PRIMS primitives of the pending leaf, their loads issued together
