@@ -730,7 +730,10 @@ BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<
     }
     for (int i = 0; i < n; i++) np += kind_of[i] == 5;
     // groups: subtrees of the SAH BVH with at most kGroupMax primitives (small scenes only)
-    int kGroupMax = 4; // die.txt 1080p grouped: 2 -> 50.1 ms, 3 -> 47.6, 4 -> 46.4, 6 -> 48.4, 8 -> 48.4, 16 -> 50.7
+    // generic kernel, die.txt 1080p grouped: 2 -> 50.1 ms, 3 -> 47.6, 4 -> 46.4, 6 -> 48.4, 8 -> 48.4, 16 -> 50.7;
+    // scene-specialised build (literal operands make primitive tests cheaper than group tests):
+    // 2 -> 32.8, 3 -> 30.6, 4 -> 30.2-30.4, 5 -> 28.9, 6 -> 29.1, 7 -> 28.3, 8 -> 28.3, 10 -> 30.2, 16 -> 30.9
+    int kGroupMax = jit_enabled() ? 8 : 4;
     if (const char* e = getenv("RTCORE_GROUP_MAX")) kGroupMax = std::max(1, atoi(e)); // tuning
     std::vector<std::vector<int>> cut;
     if ((int)all.size() <= 4096 && !sah.order.empty()) {
