@@ -30,6 +30,24 @@ void parallel_for(int n, F&& fn)
     for (auto& x : th) x.join();
 }
 
+// fn(a, b) over contiguous ranges covering [0, n) on up to 16 host threads, each range at least
+// min_items long (streaming passes over large arrays).
+template <class F>
+void parallel_ranges(size_t n, size_t min_items, F&& fn)
+{
+    const size_t hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t T = std::max<size_t>(1, std::min(std::min<size_t>(hw, 16), n / std::max<size_t>(1, min_items)));
+    if (T <= 1) {
+        fn((size_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (n + T - 1) / T;
+    for (size_t t = 0; t < T; t++)
+        th.emplace_back([&fn, t, per, n] { fn(std::min(n, t * per), std::min(n, (t + 1) * per)); });
+    for (auto& x : th) x.join();
+}
+
 // Axis-aligned box in the reference's fp64 representation (Acceleration/AABB.cs:44-64).
 struct Box {
     Vec4d mn, mx, size, ctr;

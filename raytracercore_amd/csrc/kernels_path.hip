@@ -1345,6 +1345,25 @@ __global__ void colors_1spp_kernel(PathParams p, double* out)
     out[o + 2] = miss ? -1.0 : (double)v.z;
 }
 
+// Planar row-major tile accumulators -> the caller's SampleSet order (C# [x, y]: x*h + y), so
+// that the host-buffer entry point copies one contiguous image and adds it sequentially:
+// rgb interleaved (DoubleColor), then samples, then misses.
+__global__ void tile_host_layout_kernel(int w, int h, const double* __restrict__ sum, const uint32_t* __restrict__ ns,
+                                        const uint32_t* __restrict__ ms, double* __restrict__ rgb,
+                                        uint32_t* __restrict__ on, uint32_t* __restrict__ om)
+{
+    const size_t npix = (size_t)w * h;
+    const size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= npix) return;
+    const size_t x = o / (size_t)h, y = o - x * (size_t)h;
+    const size_t i = y * (size_t)w + x;
+    rgb[3 * o + 0] = sum[i];
+    rgb[3 * o + 1] = sum[npix + i];
+    rgb[3 * o + 2] = sum[2 * npix + i];
+    on[o] = ns[i];
+    om[o] = ms[i];
+}
+
 using PathKernel = void (*)(PathScene, const CameraF*, const PathParams*, const TestRec*, const RectRec*, const FrameRec*, const PrimF*,
                             const NodeF*, const Node4Q*, const GroupRec*, const XformF*, const MatF*, const float4*);
 
@@ -1505,6 +1524,17 @@ hipError_t launch_tonemap(int w, int h, const double* d_sum, const uint32_t* d_s
     const int n = w * h;
     hipLaunchKernelGGL(tonemap_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, w, h, d_sum, d_samples, d_misses,
                        back.r, back.g, back.b, back_alpha, exposure, d_argb);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_host_layout(int w, int h, const double* d_sum, const uint32_t* d_samples,
+                                  const uint32_t* d_misses, double* d_rgb, uint32_t* d_n, uint32_t* d_m,
+                                  hipStream_t stream)
+{
+    const size_t npix = (size_t)w * h;
+    if (npix == 0) return hipSuccess;
+    hipLaunchKernelGGL(tile_host_layout_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream, w, h, d_sum,
+                       d_samples, d_misses, d_rgb, d_n, d_m);
     return hipGetLastError();
 }
 

@@ -1,0 +1,37 @@
+"""Rates through the host-buffer entry points (the PCIe-inclusive view; bench.py's `value` keeps the
+accumulators in HBM): rt_render_tile (spp samples per call into host SampleSet buffers) and
+rt_render_tile_1spp (Raytracer.Render's one-pass contract, DoubleColor[w, h] per pass), 1080p
+bounce.txt camera 0.  Prints one JSON line."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import raytracercore_amd as rc  # noqa: E402
+
+W, H = 1920, 1080
+scene = rc.SceneLoader.from_file(rc.scene_path("bounce.txt"))
+g = rc.GpuRaytracer(scene, 0, size=(W, H))
+out = {}
+for spp in (256, 16):
+    g.render_tile(0, 0, W, H, spp, seed=1)  # warm-up (buffers, specialised build)
+    t0 = time.perf_counter()
+    rays = 0
+    n = 5
+    for k in range(n):
+        s, ns, ms, r = g.render_tile(0, 0, W, H, spp, seed=1, sample_base=(k + 1) * spp)
+        rays += r
+    dt = (time.perf_counter() - t0) / n
+    out[f"render_tile_{spp}spp"] = {"ms_per_call": round(dt * 1e3, 2), "mrays_per_s": round(rays / n / dt / 1e6, 1),
+                                   "kernel_ms": round(g.last_kernel_ms(), 2)}
+g.render_tile_1spp(0, 0, W, H, seed=1, sample_index=0)
+t0 = time.perf_counter()
+n = 20
+for k in range(n):
+    g.render_tile_1spp(0, 0, W, H, seed=1, sample_index=k + 1)
+dt = (time.perf_counter() - t0) / n
+out["render_tile_1spp"] = {"ms_per_pass": round(dt * 1e3, 2), "msamples_per_s": round(W * H / dt / 1e6, 1),
+                           "kernel_ms": round(g.last_kernel_ms(), 2)}
+g.close()
+print(json.dumps(out), flush=True)
