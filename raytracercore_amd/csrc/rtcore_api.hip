@@ -2143,13 +2143,17 @@ int debug_pass_host(rt_scene* s, int mode, int32_t x0, int32_t y0, int32_t w, in
     std::vector<int32_t> tmp(npix);
     HIP_TRY(hipMemcpyAsync(tmp.data(), s->ids.p, npix * sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
-    bool overflow = false;
-    for (int y = 0; y < h; y++)
-        for (int x = 0; x < w; x++) {
-            int32_t v = tmp[(size_t)y * w + x];
-            overflow |= v == -2;
-            out[(size_t)x * h + y] = v;
-        }
+    std::atomic<bool> overflow{false};
+    parallel_ranges((size_t)w, 64, [&](size_t xa, size_t xb) { // column ranges: disjoint output spans
+        bool of = false;
+        for (int y = 0; y < h; y++)
+            for (size_t x = xa; x < xb; x++) {
+                const int32_t v = tmp[(size_t)y * w + x];
+                of |= v == -2;
+                out[x * h + y] = v;
+            }
+        if (of) overflow = true;
+    });
     if (overflow) {
         set_error(std::string(name) + ": the reference BVH is deeper than the exact kernel's traversal stack");
         return RT_ERR_STATE;
@@ -2239,17 +2243,19 @@ void scatter_band_set(const unsigned char* slot, size_t plane, int W, int H, int
     const double* hs = reinterpret_cast<const double*>(slot);
     const uint32_t* hn = reinterpret_cast<const uint32_t*>(hs + 3 * plane);
     const uint32_t* hm = hn + plane;
-    int tr = 0;
-    for (int b = offset; b * band < H; b += stride)
-        for (int y = b * band; y < std::min(H, (b + 1) * band); y++, tr++)
-            for (int x = 0; x < W; x++) {
-                const size_t i = (size_t)tr * W + x, o = (size_t)x * H + y;
-                sum_rgb[o].r += hs[i];
-                sum_rgb[o].g += hs[plane + i];
-                sum_rgb[o].b += hs[2 * plane + i];
-                samples[o] += hn[i];
-                misses[o] += hm[i];
-            }
+    parallel_ranges((size_t)W, 64, [&](size_t xa, size_t xb) { // column ranges: disjoint output spans
+        int tr = 0;
+        for (int b = offset; b * band < H; b += stride)
+            for (int y = b * band; y < std::min(H, (b + 1) * band); y++, tr++)
+                for (size_t x = xa; x < xb; x++) {
+                    const size_t i = (size_t)tr * W + x, o = x * H + y;
+                    sum_rgb[o].r += hs[i];
+                    sum_rgb[o].g += hs[plane + i];
+                    sum_rgb[o].b += hs[2 * plane + i];
+                    samples[o] += hn[i];
+                    misses[o] += hm[i];
+                }
+    });
 }
 
 // Queues one band set's render on stream: path kernel + accumulate into d_slot (added to).
