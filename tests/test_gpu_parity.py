@@ -118,6 +118,35 @@ def test_sample_level_agreement(rc, scenes):
     assert set(np.unique(g[np.all(g < 0, axis=-1)])) <= {-1.0}
 
 
+def test_host_tile_equals_device_render_1080p(rc, scenes):
+    """rt_render_tile (host arrays, SampleSet [x, y] order, added to) at the full 1080p frame equals
+    the device-resident render of the same samples, transposed, bit for bit; a second call adds."""
+    import torch
+
+    W, H, spp = 1920, 1080, 4
+    gpu = rc.GpuRaytracer(scenes["die.txt"], 0, size=(W, H))
+    dev = torch.device("cuda", 0)
+    d_sum = torch.zeros(3 * W * H, dtype=torch.float64, device=dev)
+    d_n = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    d_m = torch.zeros(W * H, dtype=torch.int32, device=dev)
+    d_r = torch.zeros(1, dtype=torch.int64, device=dev)
+    gpu.render_device(0, 0, W, H, spp, 5, 7, d_sum.data_ptr(), d_n.data_ptr(), d_m.data_ptr(), d_r.data_ptr(), 0)
+    torch.cuda.synchronize(dev)
+    s, n, m, rays = gpu.render_tile(0, 0, W, H, spp, seed=5, sample_base=7)
+    ds = d_sum.cpu().numpy().reshape(3, H, W).transpose(2, 1, 0)  # -> [x, y, rgb]
+    assert np.array_equal(s, ds)
+    assert np.array_equal(n, d_n.cpu().numpy().reshape(H, W).T.astype(np.uint32))
+    assert np.array_equal(m, d_m.cpu().numpy().reshape(H, W).T.astype(np.uint32))
+    assert rays == int(d_r.item())
+    lib, C_ = gpu.lib, __import__("ctypes")
+    r2 = C_.c_uint64(0)
+    assert lib.rt_render_tile(gpu.handle, 0, 0, W, H, spp, 5, 7, s.ctypes.data_as(C_.POINTER(rc.rt_color)),
+                              n.ctypes.data_as(C_.POINTER(C_.c_uint32)), m.ctypes.data_as(C_.POINTER(C_.c_uint32)),
+                              C_.byref(r2)) == 0
+    assert np.array_equal(s, 2 * ds) and np.all(n + m == 2 * spp) and r2.value == rays
+    gpu.close()
+
+
 def test_full_1080p_properties(rc, scenes):
     """Full configs[1] workload: bookkeeping, reproducibility, rays per sample."""
     import torch
