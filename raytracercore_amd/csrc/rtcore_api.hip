@@ -1209,9 +1209,14 @@ PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint6
     // A launch over fewer pixels than a 1080p frame takes proportionally more chunks per pixel
     // (up to 256), so that a band set of 1/N of the frame at N x the samples (bench.py on N GPUs)
     // gets items as short as one GPU's whole-frame launch, and with them the same launch tail.
-    int chunks = 32;
+    // The BVH kernels take twice as many (C4 at 64 spp: one sample per item; 16 / 32 / 64 chunks
+    // 58.7 / 55.0-55.2 / 53.7 ms): their items start in batched shading phases, so a short item
+    // costs little, and the tail of a launch of long, divergent BVH paths shrinks.
+    const int base_chunks = (s->variant >> 1) >= 2 ? 64 : 32;
+    int chunks = base_chunks;
     const double npix = (double)w * (double)h;
-    if (npix > 0 && npix < 2073600.0) chunks = (int)std::min(256.0, 32.0 * std::ceil(2073600.0 / npix));
+    if (npix > 0 && npix < 2073600.0)
+        chunks = (int)std::min(8.0 * base_chunks, base_chunks * std::ceil(2073600.0 / npix));
     if (const char* e = getenv("RTCORE_PATH_CHUNKS")) chunks = std::max(1, atoi(e));
     p.chunk = std::max(1, std::min(64, (spp + chunks - 1) / chunks));
     const int used = (spp + p.chunk - 1) / p.chunk;
