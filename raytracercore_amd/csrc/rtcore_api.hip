@@ -1217,6 +1217,11 @@ PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint6
     const double npix = (double)w * (double)h;
     if (npix > 0 && npix < 2073600.0)
         chunks = (int)std::min(8.0 * base_chunks, base_chunks * std::ceil(2073600.0 / npix));
+    // A larger frame has more items, so a relatively shorter tail: fewer, longer items then save
+    // item switches and partials (die.txt 4K x 512 spp: 8 / 16 / 32 / 64 chunks -> 55.2 / 55.6 /
+    // 56.6-57.0 / 57.0 ms kernel, 55.8 / 56.3-56.5 / 57.8-58.1 / 59.0 ms per step).
+    else if (npix > 2073600.0)
+        chunks = (int)std::max(base_chunks / 4.0, std::ceil(base_chunks * 2073600.0 / npix));
     if (const char* e = getenv("RTCORE_PATH_CHUNKS")) chunks = std::max(1, atoi(e));
     p.chunk = std::max(1, std::min(64, (spp + chunks - 1) / chunks));
     const int used = (spp + p.chunk - 1) / p.chunk;
