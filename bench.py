@@ -46,6 +46,7 @@ def load_scene(rc, scene_file):
         return rc.SceneLoader.from_text(mesh_scene_text())
     return rc.SceneLoader.from_file(rc.scene_path(scene_file))
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 vector = fp32 MFMA dense peak
+BASELINE_METRIC = "Mrays/sec (primary+secondary) and samples/sec at 1080p, Cornell box"  # BASELINE.json
 
 
 def scene_counts(scene):
@@ -56,48 +57,57 @@ def scene_counts(scene):
     return kinds.count(rc.RT_PRIM_TRIANGLE), kinds.count(rc.RT_PRIM_SPHERE), kinds.count(rc.RT_PRIM_PLANE), n_xf
 
 
-def flops_per_ray(st, scene) -> float:
-    """SURVEY.md §8(d) compute view: 20*N_node + 45*N_tri + 30*N_sph (+60 per transformed sphere) + 150,
-    with N_* the node visits / primitive tests per ray segment measured by the instrumented kernel."""
-    n_tri, n_sph, n_pln, n_xf = scene_counts(scene)
-    xf_share = n_xf / n_sph if n_sph else 0.0
-    return (20.0 * st["nodes"] + 45.0 * st["tris"] + 30.0 * st["sphs"] * (1.0 + 2.0 * xf_share)
-            + 30.0 * n_pln + 150.0)
+def flops_per_ray(st) -> float:
+    """SURVEY.md §8(d) compute view, exactly: 20*N_node + 45*N_tri + 30*N_sph + 150 FLOP per ray segment,
+    with N_* the node visits / primitive tests per ray segment measured by the instrumented kernel
+    (rectangles, boxes' faces and frame faces count as triangles; C2: 45*19 + 30*3 + 150 = 1095)."""
+    return 20.0 * st["nodes"] + 45.0 * st["tris"] + 30.0 * st["sphs"] + 150.0
 
 
 def bytes_per_ray(st, scene) -> float:
     """SURVEY.md §8(d) B_ray: 32 + 16 + 32*N_node + 48*N_tri + 16*N_sph (+144 transformed) + 48."""
     n_tri, n_sph, n_pln, n_xf = scene_counts(scene)
     xf_share = n_xf / n_sph if n_sph else 0.0
-    return 32 + 16 + 32.0 * st["nodes"] + 48.0 * st["tris"] + st["sphs"] * (16.0 + 144.0 * xf_share) + 16.0 * n_pln + 48
+    return 32 + 16 + 32.0 * st["nodes"] + 48.0 * st["tris"] + st["sphs"] * (16.0 + 144.0 * xf_share) + 48
 
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
 
 
-def roofline(cfg, fpr, bpr, rays, ms):
-    """C2/C3 (scene on chip) are bound by fp32 VALU issue; C4 (1M triangles, a
-    ~220 MB BVH + triangle set) by memory: its B_ray stream is priced against HBM."""
+def roofline(cfg, fpr, bpr, rays, ms, counters=None):
+    """C4 (1M triangles, a ~220 MB BVH + triangle set) is bound by memory: its
+    B_ray stream is priced against HBM.  C1-C3/C5 (scene on chip) are bound by fp32 VALU issue:
+    the algorithmic FLOP per ray segment x rays per launch / kernel time against the fp32 vector
+    peak.  `counters` (profiles/traffic/<config>.json, tools/pmc_summary.py over the same command)
+    adds the hardware view: SQ_INSTS_VALU_FLOPS_FP32 x 64 per launch / kernel time and the VALU
+    issue rate per SIMD-cycle."""
     secs = ms * 1e-3
     if cfg == "mesh1080":
         gbs = bpr * rays / secs / 1e9
         return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                 "note": f"SURVEY B_ray {bpr:.0f} B per ray segment (node visits and triangle tests measured by the "
-                        f"instrumented kernel) x rays per launch / path-kernel time; compute view "
-                        f"{fpr * rays / secs / 1e12:.2f} TFLOP/s of {FP32_PEAK_TFLOPS}"}
+                        f"instrumented kernel) x {rays:.4g} rays per launch / path-kernel time"}
     tf = fpr * rays / secs / 1e12
-    # the contract's compute bound is named "mfma"; the engine that bounds this kernel is the fp32
-    # VALU, whose gfx950 peak equals the fp32 MFMA dense peak (157.3 TFLOP/s)
-    return {"bound": "mfma", "engine": "valu_fp32", "achieved": round(tf, 3), "peak": FP32_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": None,
-            "note": f"fp32 VALU kernel (no MFMA instructions; the gfx950 fp32 vector and MFMA peaks are both 157.3 TFLOP/s); "
-                    f"{fpr:.0f} algorithmic FLOP per ray (SURVEY 8(d)); HBM view (SURVEY B_ray {bpr:.0f} B/ray, "
-                    f"scene served on chip): {bpr * rays / secs / 1e9:.0f} GB/s"}
+    out = {"bound": "valu_fp32", "achieved": round(tf, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+           "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": None,
+           "note": f"fp32 VALU kernel, no MFMA (gfx950 fp32 vector peak {FP32_PEAK_TFLOPS} TFLOP/s); SURVEY 8(d) "
+                   f"{fpr:.0f} FLOP per ray segment x {rays:.4g} rays per launch / path-kernel time; the scene is "
+                   f"compiled into the kernel (SGPR/literal operands), so the only HBM stream is the per-item "
+                   f"partials (traffic)"}
+    if counters and "valu_flops_fp32" in counters:
+        hw = counters["valu_flops_fp32"] * 64 / secs / 1e12
+        out["counter_view"] = {
+            "achieved": round(hw, 3), "frac": round(hw / FP32_PEAK_TFLOPS, 4), "unit": "TFLOP/s",
+            "valu_issue_per_simd_cycle": counters.get("valu_issue_per_simd_cycle"),
+            "valu_lane_utilisation": counters.get("valu_lane_utilisation"),
+            "basis": "SQ_INSTS_VALU_FLOPS_FP32 x 64 per launch (PMC, tools/pmc_summary.py) / live path-kernel time"}
+    return out
 
 
 def path_stats(gpu, W, H, spp, seed, d_rays):
-    """One untimed instrumented launch: traversal work per ray segment and the wave-cycle split."""
+    """One untimed instrumented launch: traversal work per ray segment (N_node, N_tri, N_sph of the
+    SURVEY formulas) and, for the BVH kernels, where the lane slots of the loop go."""
     import torch
 
     dev = d_rays.device
@@ -111,26 +121,62 @@ def path_stats(gpu, W, H, spp, seed, d_rays):
     st = gpu.get_stats()
     gpu.set_stats(False)
     rays = max(1, int(d_rays.item()))
-    cyc = st["cyc_start"] + st["cyc_trace"] + st["cyc_shade"]
+    # (the brute-force kernels' cycle-counter split is not reported: read on the generic STATS
+    # kernel with s_memtime around sections whose loads are still in flight, it disagreed with the
+    # duplicated-section costs of the timed kernel)
     out = {"nodes": st["node_visits"] / rays, "tris": st["tri_tests"] / rays, "sphs": st["sph_tests"] / rays,
-           "cycles": {k: round(st["cyc_" + k] / max(1, cyc), 4) for k in ("start", "trace", "shade")},
-           "wave_iters_per_ray": round(st["wave_iters"] * 64 / rays, 4)}
-    if gpu.info().traversal in (2, 3):  # BVH kernels: the three counters are lane slots, not cycles
+           "wave_iters_per_ray": round(st["wave_iters"] * 64 / rays, 4), "lane_slots": None}
+    if gpu.info().traversal in (2, 3):  # BVH kernels: the three "cycle" counters count lane slots
         slots = st["wave_iters"] * 64
         node, leaf, idle, wait = st["node_visits"], st["cyc_start"], st["cyc_trace"], st["cyc_shade"]
-        out["cycles"] = None
         out["lane_slots"] = {k: round(v / rays, 3) for k, v in (
             ("node_step", node), ("leaf_step", leaf), ("traversing_idle", idle), ("waiting_for_shading", wait),
             ("no_work", slots - node - leaf - idle - wait))}
     return out
 
 
-def cpu_baseline(cfg_name: str, threads: int):
-    """The oracle (C++ fp64 restatement of the reference algorithm) on the host cores, 4 spp."""
+def host_cores():
+    """The host CPUs this process may use (affinity mask, any cgroup CPU quota, the job's CPU share),
+    the machine's CPU count and the CPU model string (nproc and the model are recorded)."""
+    total = os.cpu_count() or 1
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = total
+    quota = None
+    try:  # cgroup v2: "max 100000" or "<quota> <period>"
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    share = None  # the CPU share a job scheduler allots (the GPU box exports it as OMP_NUM_THREADS)
+    try:
+        share = int(os.environ["OMP_NUM_THREADS"]) or None
+    except (KeyError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    threads = min(v for v in (usable, quota, share) if v)
+    return {"nproc": total, "affinity": usable, "cgroup_quota": quota, "job_share": share, "threads": threads,
+            "cpu_model": model}
+
+
+def cpu_baseline(cfg_name: str, threads: int = 0):
+    """The oracle (C++ fp64 restatement of the reference algorithm, FullRaytracer's tile passes)
+    on every host core this process may use, over a bounded sample of the workload."""
     from oracle.oracle import OracleScene
     import raytracercore_amd as rc
 
-    scene_file, cam, W, H, _ = CONFIGS[cfg_name]
+    hc = host_cores()
+    threads = threads or hc["threads"]
+    scene_file, cam, W, H, spp_cfg = CONFIGS[cfg_name]
     if scene_file == "@mesh":  # 1M triangles: the reference's collect-all-leaves query is slow, so
         from raytracercore_amd.scenes import mesh_scene_text  # a half-size frame at 1 spp
 
@@ -138,7 +184,8 @@ def cpu_baseline(cfg_name: str, threads: int):
         W, H, spp = W // 2, H // 2, 1
     else:
         orc = OracleScene.from_file(rc.scene_path(scene_file))
-        spp = 16 if W * H > 100000 else 64  # a few seconds on 16 host threads
+        # C1 (bounce256) in full; the larger frames at 16 spp (a few seconds on 16 host threads)
+        spp = spp_cfg if W * H <= 65536 else 16
     orc.set_size(W, H)
     orc.select_camera(cam)
     _, n, m, rays, secs, used = orc.render_frame(spp, seed=0, threads=threads)
@@ -147,9 +194,10 @@ def cpu_baseline(cfg_name: str, threads: int):
         "unit": "Mrays/s",
         "cores": used,
         "kind": "port",
+        "host": hc,
         "sample": f"{scene_file} camera {cam} {W}x{H} x {spp} spp (1 spp per tile pass, FullRaytracer tiling), "
-                  f"{rays} rays in {secs:.2f} s; samples/s {W * H * spp / secs:.4g}; C++ fp64 restatement, "
-                  f"not the C# binary",
+                  f"{rays} rays in {secs:.2f} s on {used} threads ({hc['cpu_model']}, nproc {hc['nproc']}); "
+                  f"samples/s {W * H * spp / secs:.4g}; C++ fp64 restatement, not the C# binary",
     }
 
 
@@ -227,10 +275,7 @@ def main() -> int:
         def start_merge(k: int):
             return k, sharding.gather_slots(slots[k % 2], glists[k % 2], dist, async_op=True)
 
-        def finish_merge(pending) -> None:
-            k, works = pending
-            for w in works:
-                w.wait()  # the compute stream waits for the gather, not the host
+        def apply_merge(k: int) -> None:
             if rank == 0:
                 got = glists[k % 2] if world > 1 else [slots[k % 2]]
                 sharding.scatter_slots(f_sum, f_n, f_m, got, rows, W, plane)
@@ -254,10 +299,7 @@ def main() -> int:
         def start_merge(k: int):
             return k, sharding.merge_accumulators(sets[k % 2], dist, async_op=True)
 
-        def finish_merge(pending) -> None:
-            k, works = pending
-            for w in works:
-                w.wait()
+        def apply_merge(k: int) -> None:
             if rank == 0:
                 d_sum, d_n, d_m = sets[k % 2]
                 f_sum.add_(d_sum)
@@ -265,6 +307,12 @@ def main() -> int:
                 f_m.add_(d_m)
         expect_per_step = spp * world
         parallelism = f"sample-sharded x{world}, " + ("RCCL reduce per step" if world > 1 else "one GPU, no collective")
+
+    def finish_merge(pending) -> None:
+        k, works = pending
+        for w in works:
+            w.wait()  # the compute stream waits for the collective, not the host
+        apply_merge(k)
 
     def run(first: int, count: int) -> list:
         # each launch records its own hipEvent pair around the path kernel (a ring of 64 per scene):
@@ -307,23 +355,72 @@ def main() -> int:
     elapsed = float(elapsed.item())
     total_rays = int(rays.item())
     total_samples = npix * spp * args.steps * world
+    avg_ms = sum(kernel_ms) / len(kernel_ms)
 
+    # bookkeeping of the timed and warm-up steps (before the untimed diagnostic steps below)
     if rank == 0:
         n_all = f_n.cpu().numpy().astype(np.int64)
         m_all = f_m.cpu().numpy().astype(np.int64)
         expect = expect_per_step * (args.steps + args.warmup)
         if not np.all(n_all + m_all == expect):
             raise SystemExit(f"sample bookkeeping mismatch: {np.unique(n_all + m_all)} != {expect}")
+
+    multi = None
+    if world > 1:
+        # where an N-GPU step's time goes, from untimed steps after the timed region: every rank's
+        # path-kernel time, and the render, collective and merge phases run one at a time
+        ks = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(ks, torch.tensor([avg_ms], dtype=torch.float64, device=dev))
+        k_all = [float(t.item()) for t in ks]
+        phases = []
+        for j in range(3):
+            k = args.warmup + args.steps + j
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            p0 = time.perf_counter()
+            step(k)
+            torch.cuda.synchronize(dev)
+            p1 = time.perf_counter()
+            dist.barrier()  # the collective starts when every rank has rendered
+            p2 = time.perf_counter()
+            _, works = start_merge(k)
+            for w in works:
+                w.wait()
+            torch.cuda.synchronize(dev)
+            p3 = time.perf_counter()
+            apply_merge(k)
+            torch.cuda.synchronize(dev)
+            p4 = time.perf_counter()
+            phases.append(torch.tensor([p1 - p0, p3 - p2, p4 - p3], dtype=torch.float64, device=dev))
+        ph = torch.stack(phases).median(dim=0).values
+        dist.all_reduce(ph, op=dist.ReduceOp.MAX)
+        multi = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
+                 "kernel_ms_per_rank": [round(v, 3) for v in k_all],
+                 "kernel_ms_min": round(min(k_all), 3), "kernel_ms_max": round(max(k_all), 3),
+                 "render_ms": round(float(ph[0]) * 1e3, 3),
+                 ("gather_ms" if args.split == "bands" else "reduce_ms"): round(float(ph[1]) * 1e3, 3),
+                 ("scatter_ms" if args.split == "bands" else "add_ms"): round(float(ph[2]) * 1e3, 3),
+                 "basis": "median of 3 untimed steps after the timed region, phases run one at a time "
+                          "(max over ranks); in the timed steps the collective of step k overlaps the "
+                          "render of step k+1"}
+
+    if rank == 0:
         my_rays_per_step = total_rays / (args.steps * world)  # the average rank's launch
-        avg_ms = sum(kernel_ms) / len(kernel_ms)
         build = gpu.build_stats()  # of the timed launches (before the instrumented one below)
         # the BVH kernels' lane-slot split depends on the launch's length (its tail), so they are
         # instrumented at the timed launch's spp; the brute-force kernels at 1/16 of it
         st = path_stats(gpu, W, H, spp if info.traversal in (2, 3) else max(1, spp // 16), args.seed, d_rays)
-        fpr = flops_per_ray(st, scene)
+        fpr = flops_per_ray(st)
         bpr = bytes_per_ray(st, scene)
+        counters = None
+        traffic_file = os.path.join(ROOT, "profiles", "traffic", f"{args.config}.json")
+        # PMC figures of this launch shape (tools/profile.sh); the profiles are of the 1-GPU launch
+        if os.path.exists(traffic_file) and args.spp == 0 and world == 1:
+            counters = json.load(open(traffic_file))
+        metric = BASELINE_METRIC if args.config == "bounce1080" else \
+            f"Mrays/sec (primary+secondary) and samples/sec, {scene_file} {W}x{H}"
         out = {
-            "metric": "Mrays/sec (primary+secondary) and samples/sec at 1080p, Cornell box",
+            "metric": metric,
             "value": round(total_rays / elapsed / 1e6, 2),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -346,17 +443,19 @@ def main() -> int:
             "published_reference": {"samples_per_s": 3.0576e6, "source": "Screenshots/app.png status bar"},
             "rays_per_sample": round(total_rays / total_samples, 4),
             "kernel_ms": round(avg_ms, 3),
-            "roofline": roofline(args.config, fpr, bpr, my_rays_per_step, avg_ms),
+            "roofline": roofline(args.config, fpr, bpr, my_rays_per_step, avg_ms, counters),
             "path_stats": {"per_ray": {k: round(st[k], 3) for k in ("nodes", "tris", "sphs")},
+                           "flop_per_ray": round(fpr, 1), "bytes_per_ray": round(bpr, 1),
+                           "rays_per_launch": round(my_rays_per_step),
                            "lane_slots_per_ray": st["wave_iters_per_ray"],
-                           **({"wave_cycles": st["cycles"]} if st["cycles"] else {"lane_slots": st["lane_slots"]})},
+                           **({"lane_slots": st["lane_slots"]} if st["lane_slots"] else {})},
+            "multi_gpu": multi,
             "scene_build": {"builder": ["auto", "host", "gpu"][info.bvh_builder],
                             **{k: round(v, 2) for k, v in build.items()}},
         }
-        traffic_file = os.path.join(ROOT, "profiles", "traffic", f"{args.config}.json")
-        if os.path.exists(traffic_file) and args.spp == 0:  # PMC bytes of this launch shape (tools/profile.sh)
+        if counters is not None:
             rf = out["roofline"]
-            rf["traffic"] = json.load(open(traffic_file))["traffic_bytes"]
+            rf["traffic"] = counters["traffic_bytes"]
             if rf["bound"] == "hbm":
                 # the measured view beside the algorithmic one (frac, the headline, is SURVEY B_ray):
                 # PMC bytes past L2 per launch / kernel time.  The ~220 MB scene fits the 256 MB
@@ -366,8 +465,7 @@ def main() -> int:
                                   "basis": "PMC 2 x FETCH_SIZE + WRITE_SIZE per launch (L2 -> fabric, includes "
                                            "Infinity Cache hits) / path-kernel time"}
         if not args.no_cpu_baseline and world == 1:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(args.config, threads)
+            out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_threads)
         print(json.dumps(out), flush=True)
     gpu.close()
     if world > 1:

@@ -170,8 +170,10 @@ typedef enum rt_bvh_builder {
    frames, [12] other triangles, [13] spheres, [14] hot wide nodes staged in LDS;
    scene-specialised kernel of the last brute-force launch (rt_set_jit): [15] status (1 in use,
    0 not used, -1 build failed: see rt_scene_get_jit_error), [16] its hiprtc compile ms (0 when
-   it came from the cache), [17] 1 if it came from the in-process or on-disk cache */
-#define RT_BUILD_STATS_COUNT 18
+   it came from the cache), [17] 1 if it came from the in-process or on-disk cache,
+   [18] primitives per group of the grouped brute-force order (fixed at creation: 8 when the
+   scene-specialised build was on then, else 4) */
+#define RT_BUILD_STATS_COUNT 19
 
 /* ---------------------------------------------------------------- library ---- */
 int rt_abi_version(void);

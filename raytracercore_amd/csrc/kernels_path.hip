@@ -543,12 +543,57 @@ __device__ __forceinline__ float one_minus_exp2_2a(float a)
     return x > -0.0625f ? series : direct;
 }
 
+// Triangle.RayTraceAVXFaster (Triangle.cs:77-146) in fp64, in the reference's operation order
+// (FMA crosses, hadd sums), on the ray that leaves a vertex-normal triangle from its own hit
+// point o = fma(e01, u, fma(e02, v, v0)) (Triangle.cs:131).  The reference's next query meets the
+// same triangle at t ~ 0 whenever the rounding residual of t is >= 0; RayHitMatches then decides
+// whether that is the same hit (Util.cs:179-192).  For a flat triangle it always is (the face
+// normal and the geometric side agree); a smooth normal (Triangle.GetNormal, :209-224) can send the
+// ray under the geometric surface, and then it is not.  The kernel evaluates the same fp64
+// expression on its own hit point.
+__device__ __noinline__ bool vn_rehit_test(const PrimD& P, double u, double v, V3 dir, bool& inside)
+{
+    const Vec4d a = P.a, e1 = P.b, e2 = P.c;
+    const double d[4] = {(double)dir.x, (double)dir.y, (double)dir.z, 0.0};
+    const double o[4] = {__builtin_fma(e1.x, u, __builtin_fma(e2.x, v, a.x)), __builtin_fma(e1.y, u, __builtin_fma(e2.y, v, a.y)),
+                         __builtin_fma(e1.z, u, __builtin_fma(e2.z, v, a.z)), __builtin_fma(e1.w, u, __builtin_fma(e2.w, v, a.w))};
+    const double off[4] = {o[0] - a.x, o[1] - a.y, o[2] - a.z, o[3] - a.w};
+    const double b1[4] = {e1.x, e1.y, e1.z, e1.w}, c2[4] = {e2.x, e2.y, e2.z, e2.w};
+    auto crs = [](const double* l, const double* r, double* out) { // SIMDHelpers.Cross
+        out[0] = __builtin_fma(l[1], r[2], -(l[2] * r[1]));
+        out[1] = __builtin_fma(l[2], r[0], -(l[0] * r[2]));
+        out[2] = __builtin_fma(l[0], r[1], -(l[1] * r[0]));
+        out[3] = __builtin_fma(l[3], r[3], -(l[3] * r[3]));
+    };
+    auto hs = [](const double* x, const double* y) { return (x[0] * y[0] + x[1] * y[1]) + (x[2] * y[2] + x[3] * y[3]); };
+    double s1[4], s2[4];
+    crs(off, b1, s1);
+    crs(d, c2, s2);
+    const double uu = hs(off, s2), vv = hs(d, s1), tt = hs(c2, s1), det = hs(b1, s2);
+    const double inv = 1.0 / det;
+    const double invz = (inv == inv) ? inv : 0.0;
+    const double u2 = uu * invz, v2 = vv * invz, t2 = tt * invz;
+    bool rej = (u2 < 0) | (v2 < 0) | (t2 < 0);
+    rej |= (P.flags & F_MIRROR) ? ((u2 > 1) | (v2 > 1)) : ((u2 + v2) > 1);
+    inside = invz < 0;
+    return !rej;
+}
+
+// The closest hit a query starts from: none, or the re-hit of a vertex-normal triangle that
+// shade() found the reference makes (encoded in Sample.prev <= -2 as -2 - sg).
+template <bool VN, class SceneT>
+__device__ __forceinline__ Best query_start(const SceneT& s, int prev)
+{
+    if (VN && s.n_vn > 0 && prev <= -2) return Best{0.0f, -2 - prev};
+    return Best{__builtin_huge_valf(), -1};
+}
+
 // One bounce of Raytracer.GetColor after the closest-hit query.  Returns 0 to continue the
 // path, 1 if the sample ended with colour `col`, 2 if it ended as a miss (Placeholder).
-template <class SceneT, class VnP, class TestP>
+template <bool VN, class SceneT, class VnP, class TestP>
 __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ prims, const MatF* __restrict__ mats,
-                                     const XformF* __restrict__ xfs, VnP vnormals, TestP tests, const Best& b,
-                                     Sample& S, V3& col)
+                                     const XformF* __restrict__ xfs, VnP vnormals, TestP tests, const PrimD* prims_d,
+                                     const Best& b, Sample& S, V3& col)
 {
     if (b.sg < 0) {
         if (S.bounce == 0 || s.ambient_miss) return 2;
@@ -581,14 +626,16 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
     pos.y = axis == 2 ? P.a.y : pos.y;
     pos.z = axis == 3 ? P.a.z : pos.z;
     V3 n = sph ? (pos - xyz(P.a)) * P.b.y : xyz(P.d);
+    float bu = 0.0f, bv = 0.0f; // vertex-normal triangle: the barycentrics of the hit
     if (fl & (F_TRANSFORMED | F_HASNORMALS)) {
         if (sph) { // ellipsoid: the world normal is an affine map of the world hit point
             n = normalize(xf_point(xfs[__float_as_int(P.b.z)].normal, pos));
         } else { // Triangle.GetNormal quirk: Normal is never set -> NaN when inside
             const VnP vn = vnormals + 3 * id;
             const TestRec R = tests[b.sg >> 1]; // barycentrics (u, v) = rows 0, 1 of M (p, 1)
-            const float u = dot4(R.r0, pos), v = dot4(R.r1, pos);
-            n = normalize(madd(xyz(vn[2]), u + v, madd(xyz(vn[1]), v, xyz(vn[0]) * u)));
+            bu = dot4(R.r0, pos);
+            bv = dot4(R.r1, pos);
+            n = normalize(madd(xyz(vn[2]), bu + bv, madd(xyz(vn[1]), bv, xyz(vn[0]) * bu)));
             if (gin) n = v3(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
         }
     }
@@ -663,6 +710,19 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
     S.o = pos;
     S.d = normalize(out_dir);
     S.prev = id;
+    if (VN && s.n_vn > 0 && kind == RT_PRIM_TRIANGLE && (fl & F_HASNORMALS)) {
+        // does the reference's next query meet this triangle again (vn_rehit_test), and is that a
+        // new hit?  Primitive.RayTrace culls it first when one-sided (Primitive.cs:56-64).  A NaN
+        // direction (a diffuse bounce about GetNormal's NaN) never gets past the BVH root
+        // (BVH.cs:301-303: far >= 0 fails), so it meets nothing.
+        bool gin2;
+        if (!__builtin_isnan(S.d.x + S.d.y + S.d.z) && vn_rehit_test(prims_d[id], (double)bu, (double)bv, S.d, gin2) &&
+            ((fl & F_TWOSIDED) || !(gin2 ^ ((fl & F_INVERT) != 0)))) {
+            const bool front = dot(out_dir, nrm) > 0.0f; // Ray.Direction . prev.Normal (false for NaN)
+            if (front ? (gin2 == gin) : (gin2 != gin))  // Inside compared after Invert on both sides
+                S.prev = -2 - ((b.sg & ~1) | (int)gin2);
+        }
+    }
     S.tint = S.tint * (new_tint * fmaxf(total, 1.0f));
     S.bounce++;
     return 0;
@@ -840,12 +900,12 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
 }
 
 // After a closest-hit query: one bounce of GetColor; a finished sample goes into the item's sums.
-template <class SceneT, class VnP, class TestP>
+template <bool VN, class SceneT, class VnP, class TestP>
 __device__ __forceinline__ void bounce(Lane& L, Sample& S, const SceneT& s, const ShadeRecs& R, VnP vnormals, TestP tests,
-                                       const Best& b)
+                                       const PrimD* prims_d, const Best& b)
 {
     V3 col;
-    const int r = shade(s, R.prims, R.mats, R.xfs, vnormals, tests, b, S, col);
+    const int r = shade<VN>(s, R.prims, R.mats, R.xfs, vnormals, tests, prims_d, b, S, col);
     if (r != 0) {
         const bool hit = r == 1;
         L.ar += hit ? col.x : 0.0f;
@@ -905,7 +965,7 @@ typedef RT_AS_CONST const PathParams ParamsC;
 
 // Brute-force megakernel: every loop iteration issues one closest-hit query per live lane
 // (the scene's records arrive through scalar loads) and shades it.
-template <bool CULL, bool LDS, bool STATS>
+template <bool CULL, bool LDS, bool STATS, bool VN>
 __device__ __forceinline__ void path_body(const CameraF* __restrict__ camp, const PathParams* __restrict__ pp)
 {
     // everything but the LDS staging is read from the launch record *pp (fill_launch) in the
@@ -975,7 +1035,7 @@ __device__ __forceinline__ void path_body(const CameraF* __restrict__ camp, cons
             const auto xf = (const RT_AS_CONST XformF*)pq->xf;
 #endif
             const auto vnormals = (const RT_AS_CONST float4*)pq->vnormals;
-            Best b{__builtin_huge_valf(), -1};
+            Best b = query_start<VN>(sc, S.prev);
 #ifdef RT_EXP_DUP_TRACE // cost experiment: a second closest-hit query from a perturbed origin
             {
                 Best b2{__builtin_huge_valf(), -1};
@@ -1000,11 +1060,11 @@ __device__ __forceinline__ void path_body(const CameraF* __restrict__ camp, cons
                 Sample S2 = S;
                 S2.rng.k0 ^= (unsigned)S.bounce;
                 V3 c2;
-                shade(sc, R.prims, R.mats, R.xfs, vnormals, tests, b, S2, c2);
+                shade<VN>(sc, R.prims, R.mats, R.xfs, vnormals, tests, pq->prims_d, b, S2, c2);
                 exp_sink += c2.x + S2.d.x;
             }
 #endif
-            bounce(L, S, sc, R, vnormals, tests, b);
+            bounce<VN>(L, S, sc, R, vnormals, tests, pq->prims_d, b);
         } else if (STATS) {
             t2 = __builtin_readcyclecounter();
         }
@@ -1020,13 +1080,13 @@ __device__ __forceinline__ void path_body(const CameraF* __restrict__ camp, cons
     flush_counts<STATS>(wave_rays, cnt, *(const ParamsC*)pp, lane);
 }
 
-template <bool CULL, bool LDS, bool STATS>
+template <bool CULL, bool LDS, bool STATS, bool VN>
 __global__ void __launch_bounds__(256, CULL ? RT_GROUPED_WAVES : RT_PATH_WAVES)
     path_kernel(PathScene, const CameraF* __restrict__ camp, const PathParams* __restrict__ pp, const TestRec*,
                 const RectRec*, const FrameRec*, const PrimF*, const NodeF*, const Node4Q*, const GroupRec*,
                 const XformF*, const MatF*, const float4*)
 {
-    path_body<CULL, LDS, STATS>(camp, pp); // the other arguments are the BVH kernels' (same launch)
+    path_body<CULL, LDS, STATS, VN>(camp, pp); // the other arguments are the BVH kernels' (same launch)
 }
 
 // BVH megakernel with decoupled traversal.  A loop iteration advances the traversing lanes by
@@ -1036,7 +1096,7 @@ __global__ void __launch_bounds__(256, CULL ? RT_GROUPED_WAVES : RT_PATH_WAVES)
 // runs only once at least p.refill lanes wait (or none is still traversing).  So one long
 // traversal no longer holds the other 63 lanes of its wave, and the divergent shading code is
 // paid once per batch of finished queries.
-template <int WIDTH, int STACK, bool LDS, bool STATS>
+template <int WIDTH, int STACK, bool LDS, bool STATS, bool VN>
 __global__ void __launch_bounds__(256, RT_BVH_WAVES)
     path_kernel_bvh(PathScene, const CameraF* __restrict__ camp, const PathParams* __restrict__ pp, const TestRec*,
                     const RectRec*, const FrameRec*, const PrimF*, const NodeF*, const Node4Q*, const GroupRec*,
@@ -1096,7 +1156,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                     const TestRec tr = tests[i];
                     hit_plane(tr, i, S.o, S.d, S.prev, b);
                 }
-                bounce(L, S, s, R, vnormals, tests, b);
+                bounce<VN>(L, S, s, R, vnormals, tests, pq->prims_d, b);
                 done = false;
             }
             refill(L, S, p, s, *cp, lane, total);
@@ -1112,7 +1172,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                     kend = k + ((~ref) & 7) + 1;
                     more = false;
                 }
-                b = Best{__builtin_huge_valf(), -1};
+                b = query_start<VN>(s, S.prev);
                 trav = true;
             }
         }
@@ -1367,30 +1427,34 @@ __global__ void tile_host_layout_kernel(int w, int h, const double* __restrict__
 using PathKernel = void (*)(PathScene, const CameraF*, const PathParams*, const TestRec*, const RectRec*, const FrameRec*, const PrimF*,
                             const NodeF*, const Node4Q*, const GroupRec*, const XformF*, const MatF*, const float4*);
 
+// vn: the scene has vertex-normal triangles (their re-hit test, vn_rehit_test, is fp64 code that
+// costs the other scenes' kernels registers, so it is compiled only into separate instances)
 template <bool CULL, bool LDS>
-PathKernel pick_brute(bool stats)
+PathKernel pick_brute(bool stats, bool vn)
 {
-    return stats ? path_kernel<CULL, LDS, true> : path_kernel<CULL, LDS, false>;
+    if (vn) return stats ? path_kernel<CULL, LDS, true, true> : path_kernel<CULL, LDS, false, true>;
+    return stats ? path_kernel<CULL, LDS, true, false> : path_kernel<CULL, LDS, false, false>;
 }
 template <int WIDTH, int STACK, bool LDS>
-PathKernel pick_bvh(bool stats)
+PathKernel pick_bvh(bool stats, bool vn)
 {
-    return stats ? path_kernel_bvh<WIDTH, STACK, LDS, true> : path_kernel_bvh<WIDTH, STACK, LDS, false>;
+    if (vn) return stats ? path_kernel_bvh<WIDTH, STACK, LDS, true, true> : path_kernel_bvh<WIDTH, STACK, LDS, false, true>;
+    return stats ? path_kernel_bvh<WIDTH, STACK, LDS, true, false> : path_kernel_bvh<WIDTH, STACK, LDS, false, false>;
 }
 
 // variant = kernel * 2 + lds; kernel 0 brute force (flat), 1 brute force (grouped, culled),
 // 2 BVH2 (24-entry LDS stack), 3 wide BVH (RT_WIDE_STACK-entry LDS stack); both overflow to global memory
-PathKernel pick(int variant, bool stats)
+PathKernel pick(int variant, bool stats, bool vn)
 {
     switch (variant) {
-    case 1: return pick_brute<false, true>(stats);
-    case 2: return pick_brute<true, false>(stats);
-    case 3: return pick_brute<true, true>(stats);
-    case 4: return pick_bvh<2, 24, false>(stats);
-    case 5: return pick_bvh<2, 24, true>(stats);
-    case 6: return pick_bvh<4, RT_WIDE_STACK, false>(stats);
-    case 7: return pick_bvh<4, RT_WIDE_STACK, true>(stats);
-    default: return pick_brute<false, false>(stats);
+    case 1: return pick_brute<false, true>(stats, vn);
+    case 2: return pick_brute<true, false>(stats, vn);
+    case 3: return pick_brute<true, true>(stats, vn);
+    case 4: return pick_bvh<2, 24, false>(stats, vn);
+    case 5: return pick_bvh<2, 24, true>(stats, vn);
+    case 6: return pick_bvh<4, RT_WIDE_STACK, false>(stats, vn);
+    case 7: return pick_bvh<4, RT_WIDE_STACK, true>(stats, vn);
+    default: return pick_brute<false, false>(stats, vn);
     }
 }
 
@@ -1405,6 +1469,7 @@ PathScene make_path_scene(const DevScene& s)
     ps.n_slots = ps.n_bvh + s.n_pln;
     ps.n_mats = s.n_mats;
     ps.n_xf = s.n_xf;
+    ps.n_vn = s.n_vn;
     ps.root = s.root;
     ps.width = s.width;
     ps.recursion = s.recursion;
@@ -1444,10 +1509,10 @@ size_t path_dyn_lds(const DevScene& s, int variant)
     return b;
 }
 
-int path_blocks_per_cu(int variant, size_t dyn_lds, bool stats)
+int path_blocks_per_cu(int variant, size_t dyn_lds, bool stats, bool vn)
 {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(pick(variant, stats)), 256,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(pick(variant, stats, vn)), 256,
                                                      dyn_lds) != hipSuccess ||
         n < 1)
         n = 1;
@@ -1483,6 +1548,7 @@ void fill_launch(const DevScene& s, int variant, PathParams& p)
     p.xf = s.xf;
     p.mats = s.mats;
     p.vnormals = s.vnormals;
+    p.prims_d = s.prims_d;
 }
 
 hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams* d_params, int variant,
@@ -1505,7 +1571,7 @@ hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams
     const float4* vn = h.vnormals;
     void* args[] = {&ps, &ca, &pa, &tests, &rects, &frames, &prims, &nodes, &nodes4, &groups, &xf, &mats, &vn};
     const size_t dyn = path_dyn_lds(s, variant);
-    return hipLaunchKernel(reinterpret_cast<const void*>(pick(variant, stats)), dim3(grid_blocks), dim3(256), args, dyn,
+    return hipLaunchKernel(reinterpret_cast<const void*>(pick(variant, stats, s.n_vn > 0)), dim3(grid_blocks), dim3(256), args, dyn,
                            stream);
 }
 
@@ -1554,6 +1620,6 @@ hipError_t launch_colors_1spp(const PathParams& p, double* d_out, hipStream_t st
 extern "C" __global__ void __launch_bounds__(256, RT_SCENE_CONST_GROUPED ? RT_GROUPED_WAVES : RT_PATH_WAVES)
     rt_path_const(const rtc::CameraF* __restrict__ camp, const rtc::PathParams* __restrict__ pp)
 {
-    rtc::path_body<RT_SCENE_CONST_GROUPED != 0, true, false>(camp, pp);
+    rtc::path_body<RT_SCENE_CONST_GROUPED != 0, true, false, RT_SCENE_CONST_VN != 0>(camp, pp);
 }
 #endif

@@ -164,6 +164,7 @@ struct PathScene {
     int32_t n_slots;             // n_bvh + n_pln (PrimF records)
     int32_t n_mats;              // MatF records (distinct materials)
     int32_t n_xf;                // XformF records
+    int32_t n_vn;                // triangles with vertex normals (Triangle.HasNormals); 0 removes their path
     int32_t n_groups;            // brute force: GroupRec records
     int32_t root;                // child reference of the BVH root
     const Node4Q* hot4;          // wide kernel: the top nodes, staged in LDS (child refs | RT_HOT_BIT)
@@ -305,6 +306,7 @@ struct DevScene {
     const float4* vnormals;     // 3 per primitive ID (HasNormals triangles)
     int32_t n_mats;             // MatF records (distinct materials)
     int32_t n_xf;               // XformF records
+    int32_t n_vn;               // triangles with vertex normals
     // exact set
     const PrimD* prims_d;
     const XformD* xf_d;

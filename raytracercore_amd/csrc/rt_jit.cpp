@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -14,6 +15,8 @@
 #include <map>
 #include <mutex>
 #include <sstream>
+#include <sys/stat.h>
+#include <sys/time.h>
 #include <unistd.h>
 
 #include "rt_jit_sources.h" // generated: kernels_path.hip and the headers it includes
@@ -58,6 +61,38 @@ std::string cache_dir()
     return "/tmp/rtcore_jit_" + std::to_string((unsigned)getuid());
 }
 
+// The disk cache holds code objects this process will load and run, so it is used only when the
+// directory is the caller's own and nobody else can write into it: created with mode 0700, and an
+// existing directory must be owned by the caller and not group- or world-writable.
+bool cache_dir_trusted(const std::string& dir, bool create)
+{
+    struct stat st;
+    if (stat(dir.c_str(), &st) != 0) {
+        if (!create) return false;
+        std::error_code ec;
+        const std::filesystem::path parent = std::filesystem::path(dir).parent_path();
+        if (!parent.empty()) std::filesystem::create_directories(parent, ec);
+        if (mkdir(dir.c_str(), 0700) != 0 && errno != EEXIST) return false;
+        if (stat(dir.c_str(), &st) != 0) return false;
+    }
+    return S_ISDIR(st.st_mode) && st.st_uid == getuid() && (st.st_mode & (S_IWGRP | S_IWOTH)) == 0;
+}
+
+// Keeps at most kDiskKeep code objects in the cache directory: the least recently used (by mtime,
+// which a cache hit refreshes) go first, so a host that moves the camera often does not grow it
+// without bound.
+constexpr size_t kDiskKeep = 64;
+void prune_cache(const std::string& dir)
+{
+    std::error_code ec;
+    std::vector<std::pair<std::filesystem::file_time_type, std::filesystem::path>> cos;
+    for (const auto& e : std::filesystem::directory_iterator(dir, ec))
+        if (e.path().extension() == ".co") cos.push_back({e.last_write_time(ec), e.path()});
+    if (cos.size() <= kDiskKeep) return;
+    std::sort(cos.begin(), cos.end());
+    for (size_t i = 0; i + kDiskKeep < cos.size(); i++) std::filesystem::remove(cos[i].second, ec);
+}
+
 bool read_file(const std::string& path, std::vector<char>& out)
 {
     std::ifstream f(path, std::ios::binary);
@@ -69,8 +104,7 @@ bool read_file(const std::string& path, std::vector<char>& out)
 void write_file_atomic(const std::string& dir, const std::string& path, const std::vector<char>& data)
 {
     std::error_code ec;
-    std::filesystem::create_directories(dir, ec);
-    if (ec) return; // the cache is an optimisation only
+    if (!cache_dir_trusted(dir, true)) return; // the cache is an optimisation only
     const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
     {
         std::ofstream f(tmp, std::ios::binary);
@@ -80,6 +114,7 @@ void write_file_atomic(const std::string& dir, const std::string& path, const st
     }
     std::filesystem::rename(tmp, path, ec);
     if (ec) std::filesystem::remove(tmp, ec);
+    prune_cache(dir);
 }
 
 // RTCORE_JIT_FLAGS: extra compiler flags for experiments (e.g. "-DRT_EXP_DUP_TRACE"), space-separated
@@ -99,6 +134,17 @@ std::string main_source(bool grouped)
            (grouped ? "1" : "0") + "\n#include \"kernels_path.hip\"\n";
 }
 
+// The compiler options of a scene-specialised build: the library's own kernel flags (Makefile
+// HIPFLAGS: no fused multiply-adds the source does not write, no SLP packing -- v_pk_* issue no
+// faster than two plain ops on gfx950), then RTCORE_JIT_FLAGS.  They are part of the cache key.
+std::vector<std::string> compile_options(const std::string& arch)
+{
+    std::vector<std::string> opts = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off",
+                                     "-fno-slp-vectorize", "-munsafe-fp-atomics"};
+    for (const std::string& f : jit_extra_flags()) opts.push_back(f);
+    return opts;
+}
+
 bool compile(const std::string& arch, const std::string& main_src, const std::string& header, std::vector<char>& code,
              std::string& err)
 {
@@ -115,13 +161,9 @@ bool compile(const std::string& arch, const std::string& main_src, const std::st
         err = "hiprtcCreateProgram failed";
         return false;
     }
-    const std::string arch_opt = "--offload-arch=" + arch;
-    // the library's own kernel flags (Makefile HIPFLAGS): no fused multiply-adds the source does not
-    // write, no SLP packing (v_pk_* issue no faster than two plain ops on gfx950)
-    std::vector<std::string> extra = jit_extra_flags();
-    std::vector<const char*> opts = {arch_opt.c_str(), "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize",
-                                     "-munsafe-fp-atomics"};
-    for (const std::string& f : extra) opts.push_back(f.c_str());
+    const std::vector<std::string> opt_s = compile_options(arch);
+    std::vector<const char*> opts;
+    for (const std::string& o : opt_s) opts.push_back(o.c_str());
     const hiprtcResult r = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
     if (r != HIPRTC_SUCCESS) {
         size_t n = 0;
@@ -195,6 +237,7 @@ std::string jit_scene_header(const PathScene& ps, const CameraF& cam, const std:
 {
     std::ostringstream o;
     o << "// generated by rt_jit.cpp: one launch's scene as constants\n#pragma once\n";
+    o << "#define RT_SCENE_CONST_VN " << (ps.n_vn > 0 ? 1 : 0) << "\n"; // vertex-normal triangles (their re-hit test)
     PathScene p = ps;
     p.hot4 = nullptr; // brute-force kernels only
     p.n_hot4 = 0;
@@ -217,14 +260,21 @@ bool jit_kernel(int device, const std::string& header, bool grouped, JitKernel& 
         return false;
     }
     const std::string arch = prop.gcnArchName;
+    // the key covers everything the code object depends on: the embedded sources, the generated
+    // header, the entry source, every compiler option, the device architecture and the compiler
+    // and runtime versions (a ROCm upgrade must not load objects built by the old compiler)
     uint64_t key = 1469598103934665603ull;
-    key = fnv1a(key, "rtcore-jit-1", 12);
+    key = fnv1a(key, "rtcore-jit-2", 12);
     key = fnv1a(key, arch.data(), arch.size());
     for (int k = 0; k < kJitSrcCount; k++) key = fnv1a(key, kJitSrcTexts[k], std::strlen(kJitSrcTexts[k]));
     key = fnv1a(key, header.data(), header.size());
     const std::string main_src = main_source(grouped);
     key = fnv1a(key, main_src.data(), main_src.size());
-    for (const std::string& f : jit_extra_flags()) key = fnv1a(key, f.data(), f.size());
+    for (const std::string& f : compile_options(arch)) key = fnv1a(key, f.data(), f.size() + 1);
+    int versions[3] = {0, 0, 0};
+    (void)hiprtcVersion(&versions[0], &versions[1]);
+    (void)hipRuntimeGetVersion(&versions[2]);
+    key = fnv1a(key, versions, sizeof versions);
 
     std::lock_guard<std::mutex> lock(g_mu);
     out = JitKernel{};
@@ -255,10 +305,11 @@ bool jit_kernel(int device, const std::string& header, bool grouped, JitKernel& 
         };
         std::vector<char> code;
         bool loaded = false;
-        if (read_file(path, code)) {
+        if (cache_dir_trusted(dir, false) && read_file(path, code)) {
             loaded = load(code);
             if (loaded) {
                 out.from_cache = true;
+                utimes(path.c_str(), nullptr); // most recently used (prune_cache)
             } else {
                 // an unusable cache file (another ROCm, a damaged disk): drop it and rebuild
                 std::error_code ec;

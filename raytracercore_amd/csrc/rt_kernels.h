@@ -48,6 +48,7 @@ struct PathParams {
     const XformF* xf;
     const MatF* mats;
     const float4* vnormals;
+    const PrimD* prims_d;       // the exact fp64 records by primitive ID (the vertex-normal re-hit test)
 };
 
 #ifndef __HIPCC_RTC__ // host-side launch interface (not part of a hiprtc-compiled kernel)
@@ -71,7 +72,7 @@ size_t path_dyn_lds(const DevScene& s, int variant); // all dynamic LDS of a var
 // The camera and the launch parameters are read from device memory (d_cam, d_params).
 hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams* d_params, int variant,
                        int grid_blocks, hipStream_t stream, bool stats);
-int path_blocks_per_cu(int variant, size_t dyn_lds, bool stats);
+int path_blocks_per_cu(int variant, size_t dyn_lds, bool stats, bool vn); // vn: scene has vertex-normal triangles
 
 // partial -> fp64 planar accumulators (d_sum planes R | G | B, each `plane` doubles apart;
 // 0 = w*h), d_samples, d_misses (row-major w*h), added to.

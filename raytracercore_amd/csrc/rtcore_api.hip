@@ -139,6 +139,7 @@ struct rt_scene {
     double ms_prepare = 0, ms_bvh = 0, ms_upload = 0;
     struct { // the flat brute-force order's decomposition (build statistics)
         int rects = 0, boxes = 0, frames = 0, frame_boxes = 0, frame_rects = 0, tris = 0, sphs = 0;
+        int group_max = 0; // primitives per group of the grouped order
     } layout;
     DevScene dev{};
     DevBuf<PrimF> prims_bf, prims_bvh;
@@ -302,6 +303,7 @@ struct BruteOrder {
 struct BruteOrders {
     BruteOrder flat, grouped;
     int nr[3] = {0, 0, 0}, nt = 0, ns = 0, np = 0;
+    int group_max = 0; // primitives per group of the grouped order (kGroupMax at creation)
     BruteLayout layout;
 };
 BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<int>& xf_index, const SahBvh& sah)
@@ -757,8 +759,12 @@ BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<
     // generic kernel, die.txt 1080p grouped: 2 -> 50.1 ms, 3 -> 47.6, 4 -> 46.4, 6 -> 48.4, 8 -> 48.4, 16 -> 50.7;
     // scene-specialised build (literal operands make primitive tests cheaper than group tests):
     // 2 -> 32.8, 3 -> 30.6, 4 -> 30.2-30.4, 5 -> 28.9, 6 -> 29.1, 7 -> 28.3, 8 -> 28.3, 10 -> 30.2, 16 -> 30.9
+    // The size is fixed here, at scene creation, by the process-wide rt_set_jit state then: a
+    // later rt_set_jit(0) leaves the generic grouped kernel on groups of 8 (correct, tuned for the
+    // specialised build); build statistic 18 (group_max) records the size chosen.
     int kGroupMax = jit_enabled() ? 8 : 4;
     if (const char* e = getenv("RTCORE_GROUP_MAX")) kGroupMax = std::max(1, atoi(e)); // tuning
+    out.group_max = kGroupMax;
     std::vector<std::vector<int>> cut;
     if ((int)all.size() <= 4096 && !sah.order.empty()) {
         std::function<void(int, std::vector<int>&)> leaves = [&](int ref, std::vector<int>& out) {
@@ -865,6 +871,7 @@ int upload_scene(rt_scene* s)
     {
         const BruteLayout& L = orders.layout;
         s->layout.rects = L.rects;
+        s->layout.group_max = orders.group_max;
         s->layout.boxes = L.boxes;
         s->layout.frames = L.frames;
         s->layout.frame_boxes = L.frame_boxes;
@@ -1070,6 +1077,8 @@ int upload_scene(rt_scene* s)
     d.vnormals = s->vnormals.p;
     d.n_mats = (int)mats.size();
     d.n_xf = (int)xf.size();
+    d.n_vn = 0;
+    for (const HostPrim& p : H) d.n_vn += (p.kind == RT_PRIM_TRIANGLE && (p.flags & F_HASNORMALS)) ? 1 : 0;
     d.prims_d = s->prims_d.p;
     d.xf_d = s->xf_d.p;
     d.ref_nodes = nullptr; // built on first use (ensure_ref_bvh)
@@ -1131,13 +1140,13 @@ int resolve_traversal(rt_scene* s)
     // the choice for A/B measurements).
     const size_t lds = path_lds_bytes(s->dev);
     const int plain = path_variant(kernel, false), staged = path_variant(kernel, true);
-    const int occ_plain = path_blocks_per_cu(plain, path_dyn_lds(s->dev, plain), false);
-    const int occ_staged = lds <= 64 * 1024 ? path_blocks_per_cu(staged, path_dyn_lds(s->dev, staged), false) : 0;
+    const int occ_plain = path_blocks_per_cu(plain, path_dyn_lds(s->dev, plain), false, s->dev.n_vn > 0);
+    const int occ_staged = lds <= 64 * 1024 ? path_blocks_per_cu(staged, path_dyn_lds(s->dev, staged), false, s->dev.n_vn > 0) : 0;
     bool use_lds = occ_staged >= occ_plain;
     if (const char* e = getenv("RTCORE_PATH_LDS")) use_lds = e[0] == '1' && occ_staged > 0;
     s->variant = use_lds ? staged : plain;
     s->blocks_per_cu = use_lds ? occ_staged : occ_plain;
-    if (s->stats_on) s->stats_blocks_per_cu = path_blocks_per_cu(s->variant, path_dyn_lds(s->dev, s->variant), true);
+    if (s->stats_on) s->stats_blocks_per_cu = path_blocks_per_cu(s->variant, path_dyn_lds(s->dev, s->variant), true, s->dev.n_vn > 0);
     return RT_OK;
 }
 
@@ -1162,7 +1171,7 @@ int calibrate_grouping(rt_scene* s)
     const int saved_variant = s->variant, saved_blocks = s->blocks_per_cu;
     const int variant = path_variant(1, false);
     s->variant = variant;
-    s->blocks_per_cu = path_blocks_per_cu(variant, 0, true);
+    s->blocks_per_cu = path_blocks_per_cu(variant, 0, true, s->dev.n_vn > 0);
     HIP_TRY(s->stats_buf.reserve(RT_STATS_COUNT));
     HIP_TRY(s->sum.reserve((size_t)3 * w * h));
     HIP_TRY(s->samples.reserve((size_t)w * h));
@@ -1207,7 +1216,8 @@ PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint6
     // a few chunks per pixel keep the tail of a launch short while each lane still amortises
     // its item fetch over many samples (RTCORE_PATH_CHUNKS overrides the count, for tuning).
     // A launch over fewer pixels than a 1080p frame takes proportionally more chunks per pixel
-    // (up to 256), so that a band set of 1/N of the frame at N x the samples (bench.py on N GPUs)
+    // (up to 8 x the base count: 256 for the brute-force kernels, 512 for the BVH kernels; the
+    // partial buffer is 16 B x chunks x padded pixels), so that a band set of 1/N of the frame at N x the samples (bench.py on N GPUs)
     // gets items as short as one GPU's whole-frame launch, and with them the same launch tail.
     // The BVH kernels take twice as many (C4 at 64 spp: one sample per item; 16 / 32 / 64 chunks
     // 58.7 / 55.0-55.2 / 53.7 ms): their items start in batched shading phases, so a short item
@@ -1341,6 +1351,8 @@ int prepare_jit(rt_scene* s)
     if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, k.fn, 256, path_dyn_lds(s->dev, s->variant)) !=
             hipSuccess ||
         n < 1) {
+        jit_release(s->device, k.fn); // the reference jit_kernel took: the module stays evictable
+        (void)hipGetLastError();
         s->jit.status = -1;
         s->jit.error = "occupancy query of the scene-specialised kernel failed";
         return 0;
@@ -1633,7 +1645,7 @@ int rt_scene_get_build_stats(const rt_scene* s, double* out, int32_t n)
                                            (double)L.rects, (double)L.boxes, (double)L.frames, (double)L.frame_boxes,
                                            (double)L.frame_rects, (double)L.tris, (double)L.sphs,
                                            (double)s->dev.n_hot4, (double)s->jit.status, s->jit.compile_ms,
-                                           s->jit.from_cache ? 1.0 : 0.0};
+                                           s->jit.from_cache ? 1.0 : 0.0, (double)L.group_max};
     for (int i = 0; i < n && i < RT_BUILD_STATS_COUNT; i++) out[i] = v[i];
     return RT_OK;
 }
@@ -2013,7 +2025,7 @@ int rt_scene_set_stats(rt_scene* s, int32_t enable)
     if (enable) {
         HIP_TRY(s->stats_buf.reserve(RT_STATS_COUNT));
         HIP_TRY(hipMemset(s->stats_buf.p, 0, RT_STATS_COUNT * sizeof(unsigned long long)));
-        s->stats_blocks_per_cu = path_blocks_per_cu(s->variant, path_dyn_lds(s->dev, s->variant), true);
+        s->stats_blocks_per_cu = path_blocks_per_cu(s->variant, path_dyn_lds(s->dev, s->variant), true, s->dev.n_vn > 0);
     }
     s->stats_on = enable != 0;
     return RT_OK;

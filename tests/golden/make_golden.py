@@ -49,6 +49,19 @@ def screenshots(src: str):
         np.savez_compressed(os.path.join(HERE, f"screenshot_{key}.npz"), rgba=sub, xs=xs, ys=ys,
                             size=np.array([img.shape[1], img.shape[0]]))
         print(fname, sub.shape)
+    # Screenshots/app.png: the WinForms window rendering bounce.txt (camera 0, 700x700, recursion 10)
+    # at UI exposure 1.000 after 4,826.37 spp (status bar).  The 700x700 viewport sits at (4, 85) of
+    # the window (coverage agreement with the oracle's primary-ID map 0.995, best over nearby
+    # offsets); misses are transparent (background alpha 0) over the panel grey (240, 240, 240).
+    img = np.asarray(Image.open(os.path.join(src, "app.png")))[..., :3]
+    ox, oy, step = 4, 85, 8
+    view = img[oy:oy + 700, ox:ox + 700]
+    ys = np.arange(step // 2, 700, step)
+    xs = np.arange(step // 2, 700, step)
+    np.savez_compressed(os.path.join(HERE, "screenshot_app_bounce700.npz"), rgb=view[np.ix_(ys, xs)], xs=xs, ys=ys,
+                        size=np.array([700, 700]), offset=np.array([ox, oy]), exposure=np.array([1.0]),
+                        spp=np.array([4826.37]), panel=np.array([240, 240, 240]))
+    print("app.png viewport", view[np.ix_(ys, xs)].shape)
 
 
 if __name__ == "__main__":

@@ -35,6 +35,10 @@ def test_bench_line_single_gpu():
     assert 0 < rf["frac"] < 1 and rf["achieved"] == pytest.approx(rf["frac"] * rf["peak"], rel=1e-2)
     cb = d["cpu_baseline"]
     assert {"value", "unit", "cores", "kind", "sample"} <= set(cb) and cb["value"] > 0 and cb["kind"] == "port"
+    assert cb["host"]["nproc"] >= cb["cores"] >= 1 and cb["host"]["cpu_model"]
+    # C2 is VALU-bound: SURVEY 8(d)'s FLOP formula (1095 per ray segment on bounce.txt's flat order)
+    assert rf["bound"] == "valu_fp32" and d["path_stats"]["flop_per_ray"] == pytest.approx(1095, abs=1)
+    assert d["multi_gpu"] is None
     # value: rays over the timed wall clock; kernel time is within it
     assert d["kernel_ms"] <= d["ms_per_step"] * 1.001
 
@@ -49,3 +53,6 @@ def test_bench_two_ranks_one_device():
     d = _last_json(r.stdout)
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert "x2" in d["config"]["parallelism"]
+    mg = d["multi_gpu"]  # the N > 1 line explains itself: ranks' kernel times, collective and merge phases
+    assert mg["world_size"] == 2 and len(mg["kernel_ms_per_rank"]) == 2
+    assert mg["kernel_ms_min"] <= mg["kernel_ms_max"] and mg["gather_ms"] >= 0 and mg["scatter_ms"] >= 0

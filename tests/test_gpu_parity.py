@@ -373,6 +373,21 @@ def test_band_sets_device_gather_layout(rc, scenes, world):
     assert int(d_r.item()) == r2
 
 
+def test_frame_refuses_more_gpus_than_devices(rc, scenes):
+    """rt_frame_create / rt_render_frame_multi with more GPUs than rt_device_count(): RT_ERR_NODEVICE
+    with a message, no communicator attempted; the library still renders afterwards."""
+    n = rc.device_count()
+    for bad in (n + 1, 64):
+        with pytest.raises(rc.RtError, match="error -"):
+            rc.GpuFrame(scenes["die.txt"], 0, n_gpus=bad, size=(32, 24))
+        with pytest.raises(rc.RtError):
+            rc.render_frame_multi(scenes["die.txt"], 0, bad, 2, size=(32, 24))
+    f = rc.GpuFrame(scenes["die.txt"], 0, n_gpus=1, size=(32, 24))
+    s, n_, m, r = f.render(2, seed=1)
+    f.close()
+    assert (n_ + m == 2).all() and r > 0
+
+
 def test_frame_progressive_sample_base(rc, scenes):
     """A persistent rt_frame called twice with disjoint sample ranges accumulates the same samples
     as one call over both ranges (FullRaytracer's progressive refinement)."""
@@ -708,12 +723,16 @@ def test_random_box_scenes_agree(rc, seed):
 
 
 @pytest.mark.parametrize("name,mode", [("bounce.txt", "BRUTE"), ("die.txt", "GROUPED"), ("die.txt", "BRUTE"),
-                                       ("BOXES3", "BRUTE"), ("BOXES5", "GROUPED")])
+                                       ("BOXES3", "BRUTE"), ("BOXES5", "GROUPED"), ("VN", "BRUTE")])
 def test_scene_specialised_kernel_matches_generic(rc, scenes, name, mode):
     """The hiprtc build with the scene's records as constants (rt_set_jit) computes exactly what the
     generic brute-force kernel computes: bit-identical sums, counts and ray totals."""
     if name.startswith("BOXES"):
         scene = rc.SceneLoader.from_text(_random_box_scene(int(name[5:])))
+    elif name == "VN":  # vertex-normal triangles: the kernels' fp64 re-hit test (vn_rehit_test)
+        from test_gpu_oracle_paths import VN_SCENE
+
+        scene = rc.SceneLoader.from_text(VN_SCENE)
     else:
         scene = scenes[name]
     trav = getattr(rc, "RT_TRAVERSAL_" + mode)
@@ -807,22 +826,28 @@ g.close()
 """
 
 
-def test_scene_specialised_cache_file_damage_recovers(tmp_path):
-    """The on-disk code-object cache: a second process loads the first one's build; a damaged cache
-    file is dropped and rebuilt, never fatal. Each probe runs in a fresh child process so the
-    in-process module cache does not hide the disk."""
+def _cache_probe(cache_dir, salt):
+    """One scene-specialised render in a fresh child process (so the in-process module cache does
+    not hide the disk), with the code-object cache in cache_dir."""
     import json
     import subprocess
     import sys
 
-    env = dict(os.environ, RTCORE_JIT_CACHE=str(tmp_path), RTCORE_JIT_FLAGS="-DRT_CACHE_TEST_SALT=1")
+    env = dict(os.environ, RTCORE_JIT_CACHE=str(cache_dir), RTCORE_JIT_FLAGS=f"-DRT_CACHE_TEST_SALT={salt}")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _CACHE_PROBE], env=env, cwd=root, capture_output=True, text=True,
+                       timeout=150)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_scene_specialised_cache_file_damage_recovers(tmp_path):
+    """The on-disk code-object cache: a second process loads the first one's build; a damaged cache
+    file is dropped and rebuilt, never fatal."""
+    os.chmod(tmp_path, 0o700)
 
     def probe():
-        r = subprocess.run([sys.executable, "-c", _CACHE_PROBE], env=env, cwd=root, capture_output=True,
-                           text=True, timeout=150)
-        assert r.returncode == 0, r.stderr[-2000:]
-        return json.loads(r.stdout.strip().splitlines()[-1])
+        return _cache_probe(tmp_path, 1)
 
     first = probe()
     assert first["status"] == 1.0 and first["cached"] == 0.0, first
@@ -837,3 +862,23 @@ def test_scene_specialised_cache_file_damage_recovers(tmp_path):
     for r in (second, third):
         assert r["rays"] == first["rays"] and r["sum"] == first["sum"]
     assert os.path.getsize(tmp_path / files[0]) > 4096  # rewritten with the fresh build
+
+
+def test_scene_specialised_cache_untrusted_dir_is_not_used(tmp_path):
+    """A cache directory others can write into is neither read nor written: every process builds
+    afresh (a planted code object would otherwise be loaded and run); a new directory is created
+    private (0700)."""
+    import stat
+
+    shared = tmp_path / "shared"
+    shared.mkdir()
+    os.chmod(shared, 0o777)
+    for _ in range(2):
+        r = _cache_probe(shared, 2)
+        assert r["status"] == 1.0 and r["cached"] == 0.0, r
+    assert not [f for f in os.listdir(shared) if f.endswith(".co")]
+    fresh = tmp_path / "new" / "cache"
+    r = _cache_probe(fresh, 3)
+    assert r["status"] == 1.0 and stat.S_IMODE(os.stat(fresh).st_mode) == 0o700
+    assert len([f for f in os.listdir(fresh) if f.endswith(".co")]) == 1
+    assert _cache_probe(fresh, 3)["cached"] == 1.0

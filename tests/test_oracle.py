@@ -125,6 +125,27 @@ def test_threaded_frame_matches_sequential():
     assert np.allclose(a[0], b[0], rtol=1e-12, atol=0)
 
 
+def test_c1_plumbing_config():
+    """BASELINE configs[0] (C1): bounce.txt 256x256 x 16 spp, camera 0, on the oracle's FullRaytracer
+    restatement (T threads, TilesY = floor(sqrt(T)), TilesX = T / TilesY, 1 spp per tile pass,
+    FullRaytracer.cs:66-72, 219-229): every pixel gets 16 samples, the result does not depend on
+    the thread count (1 vs all host cores), a pixel mean is the same whatever the tiling, and the
+    ray count per sample lies in [1, Recursion + 1]."""
+    import os
+
+    s = _scene("bounce.txt")
+    s.set_size(256, 256)
+    s.select_camera(0)
+    a = s.render_frame(16, seed=0, threads=os.cpu_count() or 1)
+    b = s.render_frame(16, seed=0, threads=1)
+    assert np.all(a[1] + a[2] == 16)
+    assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and a[3] == b[3]
+    assert np.array_equal(a[0], b[0])
+    assert 256 * 256 * 16 <= a[3] <= 256 * 256 * 16 * 11
+    t = s.render_tile(100, 120, 16, 16, 16, seed=0)
+    assert np.array_equal(t[0], a[0][100:116, 120:136])
+
+
 def _h32(x):
     x &= 0xFFFFFFFF
     x ^= x >> 16
