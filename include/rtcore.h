@@ -217,6 +217,18 @@ int rt_scene_check_bvh(rt_scene* scene);
    order's group count and its slot count.  Copies min(n_out, 10) values. */
 #define RT_LAYOUT_COUNT 10
 int rt_debug_brute_layout(const rt_prim* prims, int32_t n_prims, int32_t* out, int32_t n_out);
+/* Measurement of a wavefront split's traversal stage.  rt_debug_ray_log: while
+   the instrumented kernel runs (rt_scene_set_stats), the BVH kernels append every finished query
+   to d_log as 3 float4 (origin, previous primitive ID | direction, frame pixel index | closest t,
+   hit slot, bounce) at the
+   device counter *d_count, up to cap records (d_log = NULL turns logging off).
+   rt_debug_trace_rays: the trace-only kernel (wide BVH, no shading) over n logged queries on
+   `stream`, with waves_per_simd 6, 7 or 8; writes (t, slot) per query to d_hits, optional
+   counters to d_stats[3] (node-step lane slots, leaf-step lane slots, lane slots in all) and the
+   kernel's time (hipEvents) to *ms.  BVH traversal modes of a scene without planes only. */
+int rt_debug_ray_log(rt_scene* scene, void* d_log, uint32_t cap, void* d_count);
+int rt_debug_trace_rays(rt_scene* scene, const void* d_rays, uint32_t n, void* d_hits, int32_t waves_per_simd,
+                        void* d_stats, void* stream, float* ms);
 
 /* ------------------------------------------------------- host-buffer renders --- */
 /*

@@ -166,6 +166,9 @@ def load_library(path: str = "") -> C.CDLL:
                                         C.c_double, C.c_void_p, C.c_void_p]),
         "rt_ref_bvh_export": (C.c_int, [P(rt_prim), C.c_int32, P(C.c_int32), P(C.c_double), P(C.c_int32),
                                         P(C.c_int32)]),
+        "rt_debug_ray_log": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
+        "rt_debug_trace_rays": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_int32, C.c_void_p,
+                                          C.c_void_p, P(C.c_float)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

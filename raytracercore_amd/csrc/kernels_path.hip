@@ -96,8 +96,8 @@ __device__ __forceinline__ void hit_sph(const TestRec& R, int slot, V3 o, V3 d, 
     const float bb = dot(oc, dd);
     const V3 l = madd(dd, -bb, oc);
     const float disc = R.r1.x - dot(l, l);
-    const float sq = fsqrt(fmaxf(disc, 0.0f));
     const bool self = id == prev;
+    const float sq = fsqrt(fmaxf(disc, 0.0f));
     // self-hit: the root at the bounce point is skipped; the other root is -2 (oc.dd)
     const float tn = self ? -1.0f : -bb - sq;
     const float tf = self ? -2.0f * bb : sq - bb;
@@ -211,14 +211,15 @@ __device__ __forceinline__ void hit_box(const BoxRec& B, V3 o, V3 d, V3 id, V3 o
     int fe = 0, fo = 0;
     if (keep & 0x3Fu) { // some face keeps entry hits (wave-uniform)
         fe = te == nx ? sx : (te == ny ? 2 + sy : 4 + sz);
-        // the keep bit is tested unconditionally: selecting on "every face keeps" cost more
+        // the keep bit is tested unless every face keeps (a constant in a scene-specialised build;
+        // selecting on it at run time cost more than the test)
         ok_e = meet & (__float_as_uint(te) < __float_as_uint(b.t)) & (((perm >> (4 * fe)) & 15u) != rel_prev) &
-               (((keep >> fe) & 1u) != 0);
+               ((keep & 0x3Fu) == 0x3Fu || ((keep >> fe) & 1u) != 0);
     }
     if (keep & 0x3F00u) { // some face keeps exit hits
         fo = tx == fx ? 1 - sx : (tx == fy ? 3 - sy : 5 - sz);
         ok_x = meet & (__float_as_uint(tx) < __float_as_uint(b.t)) & (((perm >> (4 * fo)) & 15u) != rel_prev) &
-               (((keep >> (8 + fo)) & 1u) != 0);
+               ((keep & 0x3F00u) == 0x3F00u || ((keep >> (8 + fo)) & 1u) != 0);
     }
     const bool ok = ok_e | ok_x;
     b.t = ok ? (ok_e ? te : tx) : b.t;
@@ -619,7 +620,7 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
     // (world point o + t d; flat kinds carry their face normal in P.d, spheres 1/r in P.b.y), with
     // transformed spheres and vertex-normal triangles on a separate (rare) path
     V3 pos = madd(S.d, b.t, S.o);
-    const bool sph = kind == RT_PRIM_SPHERE;
+    const bool sph = (s.facts & FACT_SPHERE) && kind == RT_PRIM_SPHERE;
     const uint32_t axis = (fl & F_AXIS_MASK) >> F_AXIS_SHIFT; // axis-aligned rectangle: on its plane
     if (axis | (fl & F_FRAME_RECT)) gin = dot(S.d, xyz(P.d)) > 0.0f; // Moller-Trumbore's inside = d . N > 0
     pos.x = axis == 1 ? P.a.x : pos.x;
@@ -627,7 +628,7 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
     pos.z = axis == 3 ? P.a.z : pos.z;
     V3 n = sph ? (pos - xyz(P.a)) * P.b.y : xyz(P.d);
     float bu = 0.0f, bv = 0.0f; // vertex-normal triangle: the barycentrics of the hit
-    if (fl & (F_TRANSFORMED | F_HASNORMALS)) {
+    if ((s.facts & FACT_XF_VN) && (fl & (F_TRANSFORMED | F_HASNORMALS))) {
         if (sph) { // ellipsoid: the world normal is an affine map of the world hit point
             n = normalize(xf_point(xfs[__float_as_int(P.b.z)].normal, pos));
         } else { // Triangle.GetNormal quirk: Normal is never set -> NaN when inside
@@ -645,7 +646,7 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
     // RandomShine (Raytracer.cs:51-56): z = U^(1/shininess), theta = U * 2pi
     const float shin = M.shininess;
     float z = 1.0f, sz = 0.0f;
-    if (!(__builtin_isinf(shin) && shin > 0.0f)) {
+    if (!(s.facts & FACT_INF_SHININESS) || !(__builtin_isinf(shin) && shin > 0.0f)) {
         const float a = __builtin_amdgcn_logf(next_u(S.rng)) * M.inv_shininess; // log2(U) / shininess
         z = __builtin_amdgcn_exp2f(a);
         sz = fsqrt(one_minus_exp2_2a(a));
@@ -657,7 +658,8 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
     float spec_lum = M.specular.w, refr_lum = M.refraction.w;
     const float cs = -dot(rough, S.d);
     float cos_out = 0.0f, ior_ratio = 0.0f;
-    if (((refr_lum > 0.0f) | (spec_lum > 0.0f)) && M.ior != 0.0f && cs >= 0.0f) { // Raytracer.cs:120-161
+    if ((s.facts & FACT_IOR) && ((refr_lum > 0.0f) | (spec_lum > 0.0f)) && M.ior != 0.0f &&
+        cs >= 0.0f) { // Raytracer.cs:120-161
         ior_ratio = inside ? M.eta_exit : M.eta_enter; // eta = iorIn / iorOut
         const float sin_out = ior_ratio * fsqrt(1.0f - cs * cs);
         if (sin_out >= 1.0f) {
@@ -1156,6 +1158,15 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                     const TestRec tr = tests[i];
                     hit_plane(tr, i, S.o, S.d, S.prev, b);
                 }
+                if (STATS && p.ray_log) { // rt_debug_ray_log: the query and its closest hit
+                    const unsigned q = atomicAdd(p.ray_log_n, 1u);
+                    if (q < p.ray_log_cap) {
+                        float4* r = p.ray_log + 3 * (size_t)q;
+                        r[0] = make_float4(S.o.x, S.o.y, S.o.z, __int_as_float(S.prev));
+                        r[1] = make_float4(S.d.x, S.d.y, S.d.z, __int_as_float(L.fy * p.scene.width + L.fx));
+                        r[2] = make_float4(b.t, __int_as_float(b.sg), __int_as_float(S.bounce), 0.0f);
+                    }
+                }
                 bounce<VN>(L, S, s, R, vnormals, tests, pq->prims_d, b);
                 done = false;
             }
@@ -1327,6 +1338,122 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
 }
 
 #ifndef __HIPCC_RTC__ // the host side and the other kernels (not part of a hiprtc build)
+// Trace-only kernel (rt_debug_trace_rays): the wide BVH kernel's speculative traversal over a
+// list of logged queries, with no shading phase and no path state, so that each lane takes the
+// next ray as soon as its query ends.  It measures the traversal stage of a wavefront split
+// (Laine, Karras & Aila 2013) against the megakernel on the same rays.
+template <int STACK, int WAVES, bool STATS>
+__global__ void __launch_bounds__(256, WAVES) trace_rays_kernel(TraceRaysParams p)
+{
+    __shared__ int stack_mem[STACK * 256];
+    const TravStack stk{stack_mem + threadIdx.x, p.stack_ovf + blockIdx.x * 256 + threadIdx.x, (int)gridDim.x * 256};
+    const int lane = threadIdx.x & 63;
+    const RT_AS_CONST TestRec* tests = (const RT_AS_CONST TestRec*)p.tests;
+    const RT_AS_CONST Node4Q* nodes4 = (const RT_AS_CONST Node4Q*)p.nodes4;
+    const RT_AS_CONST XformF* xf = (const RT_AS_CONST XformF*)p.xf;
+    bool trav = false, more = false, exhausted = false;
+    int ref = 0, sp = 0, k = 0, kend = 0, prev = -1;
+    unsigned idx = 0, pool_next = 0, pool_end = 0; // the wave's pool of ray indices (uniform)
+    V3 o{0, 0, 0}, d{0, 0, 0}, id{0, 0, 0}, oi{0, 0, 0};
+    Best b{__builtin_huge_valf(), -1};
+    unsigned long long n_node = 0, n_leaf = 0, n_slots = 0;
+    while (true) {
+        const bool need = !trav && !exhausted;
+        const unsigned long long m = __ballot(need);
+        if (m) { // lanes without a query take the next rays (one atomic per 256 rays per wave)
+            const unsigned kk = (unsigned)__popcll(m), avail = pool_end - pool_next;
+            unsigned fresh = 0;
+            if (kk > avail) {
+                if (lane == 0) fresh = atomicAdd(p.counter, 256u);
+                fresh = __builtin_amdgcn_readfirstlane(fresh);
+            }
+            if (need) {
+                const unsigned r = (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+                idx = r < avail ? pool_next + r : fresh + (r - avail);
+                if (idx >= p.n) {
+                    exhausted = true;
+                } else {
+                    const float4 r0 = p.rays[3 * (size_t)idx], r1 = p.rays[3 * (size_t)idx + 1];
+                    o = v3(r0.x, r0.y, r0.z);
+                    d = v3(r1.x, r1.y, r1.z);
+                    prev = __float_as_int(r0.w);
+                    id = v3(slab_rcp(d.x), slab_rcp(d.y), slab_rcp(d.z));
+                    oi = o * id;
+                    ref = p.root4;
+                    sp = 0;
+                    k = kend = 0;
+                    more = true;
+                    if (ref < 0) {
+                        k = (~ref) >> 3;
+                        kend = k + ((~ref) & 7) + 1;
+                        more = false;
+                    }
+                    b = Best{__builtin_huge_valf(), -1};
+                    trav = true;
+                }
+            }
+            if (kk > avail) {
+                pool_next = fresh + (kk - avail);
+                pool_end = fresh + 256u;
+            } else {
+                pool_next += kk;
+            }
+        }
+        if (!__any(trav)) break;
+        const bool can_node = trav && more && ref >= 0;
+        const bool blocked = trav && k < kend && !can_node;
+        const bool leaf_step = __ballot(can_node) == 0 || __popcll(__ballot(blocked)) >= p.spec;
+        if (STATS) {
+            n_slots += 64;
+            if (leaf_step) n_leaf += (trav && k < kend) ? 1 : 0;
+            else n_node += can_node ? 1 : 0;
+        }
+        if (trav) {
+            if (leaf_step) {
+                if (k < kend) {
+                    TestRec r[RT_SPEC_PRIMS];
+#pragma unroll
+                    for (int j = 0; j < RT_SPEC_PRIMS; j++) r[j] = tests[k + j];
+#pragma unroll
+                    for (int j = 0; j < RT_SPEC_PRIMS; j++)
+                        if (j == 0 || k + j < kend) hit_any(r[j], k + j, o, d, prev, xf, b);
+                    k += RT_SPEC_PRIMS;
+                }
+            } else if (can_node) {
+                bool pop = true;
+                const Node4Q q = nodes4[ref];
+                wide_visit<STACK>(q, id, oi, b.t, ref, sp, stk, pop);
+                if (pop) {
+                    if (sp > 0) ref = pop_ref<STACK>(stk, sp);
+                    else more = false;
+                }
+            }
+            if (more && ref < 0 && k >= kend) {
+                const int code = ~ref;
+                k = code >> 3;
+                kend = k + (code & 7) + 1;
+                if (sp > 0) ref = pop_ref<STACK>(stk, sp);
+                else more = false;
+            }
+            if (!more && k >= kend) {
+                trav = false;
+                p.hits[idx] = make_float2(b.t, __int_as_float(b.sg));
+            }
+        }
+    }
+    if (STATS) {
+        for (int off = 32; off > 0; off >>= 1) {
+            n_node += __shfl_down(n_node, off);
+            n_leaf += __shfl_down(n_leaf, off);
+        }
+        if (lane == 0) {
+            atomicAdd(p.stats + 0, n_node);
+            atomicAdd(p.stats + 1, n_leaf);
+            atomicAdd(p.stats + 2, n_slots);
+        }
+    }
+}
+
 // plane: element stride between the R, G and B planes of sum (>= w*h; a gather slot may be taller
 // than the band set written into it)
 __global__ void accumulate_kernel(PathParams p, double* sum, uint32_t* samples, uint32_t* misses, size_t plane)
@@ -1470,6 +1597,7 @@ PathScene make_path_scene(const DevScene& s)
     ps.n_mats = s.n_mats;
     ps.n_xf = s.n_xf;
     ps.n_vn = s.n_vn;
+    ps.facts = s.facts;
     ps.root = s.root;
     ps.width = s.width;
     ps.recursion = s.recursion;
@@ -1601,6 +1729,30 @@ hipError_t launch_tile_host_layout(int w, int h, const double* d_sum, const uint
     if (npix == 0) return hipSuccess;
     hipLaunchKernelGGL(tile_host_layout_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream, w, h, d_sum,
                        d_samples, d_misses, d_rgb, d_n, d_m);
+    return hipGetLastError();
+}
+
+using TraceKernel = void (*)(TraceRaysParams);
+TraceKernel pick_trace(int waves, bool stats)
+{
+    if (waves >= 8) return stats ? trace_rays_kernel<16, 8, true> : trace_rays_kernel<16, 8, false>;
+    if (waves == 7) return stats ? trace_rays_kernel<16, 7, true> : trace_rays_kernel<16, 7, false>;
+    return stats ? trace_rays_kernel<20, 6, true> : trace_rays_kernel<20, 6, false>;
+}
+
+int trace_rays_blocks_per_cu(int waves)
+{
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(pick_trace(waves, false)), 256, 0) !=
+            hipSuccess ||
+        n < 1)
+        n = 1;
+    return n;
+}
+
+hipError_t launch_trace_rays(const TraceRaysParams& p, int waves, int grid_blocks, hipStream_t stream)
+{
+    hipLaunchKernelGGL(pick_trace(waves, p.stats != nullptr), dim3(grid_blocks), dim3(256), 0, stream, p);
     return hipGetLastError();
 }
 

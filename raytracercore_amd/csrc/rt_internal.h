@@ -30,6 +30,17 @@ enum : uint32_t {
     F_FRAME_RECT = 1u << 9, // brute-force slot tested as a rectangle of a FrameRec (shading: Inside from N . d)
 };
 
+// Scene facts (PathScene.facts): what the scene's primitives and materials use at all.  In a
+// scene-specialised build they are constants, so the shading code of features the scene does not
+// use (Fresnel, infinite shininess, ellipsoid and vertex normals, sphere normals) folds away.
+enum : uint32_t {
+    FACT_INF_SHININESS = 1u << 0, // some material has Shininess = +inf (RandomShine draws no z)
+    FACT_IOR = 1u << 1,           // some material has a RefractiveIndex (Fresnel / TIR)
+    FACT_XF_VN = 1u << 2,         // a transformed sphere or a vertex-normal triangle
+    FACT_SPHERE = 1u << 3,        // some sphere
+    FACT_ALL = 0xFu,
+};
+
 // Axis-aligned rectangle (a Mirror parallelogram whose edges follow two coordinate axes, e.g.
 // every Cube face, Cube.cs:90-116): the plane coordinate on `axis`, the extents on the two
 // other axes (in x, y, z order) and the one-sided culling rule folded into one factor:
@@ -165,6 +176,7 @@ struct PathScene {
     int32_t n_mats;              // MatF records (distinct materials)
     int32_t n_xf;                // XformF records
     int32_t n_vn;                // triangles with vertex normals (Triangle.HasNormals); 0 removes their path
+    uint32_t facts;              // FACT_* of the scene
     int32_t n_groups;            // brute force: GroupRec records
     int32_t root;                // child reference of the BVH root
     const Node4Q* hot4;          // wide kernel: the top nodes, staged in LDS (child refs | RT_HOT_BIT)
@@ -307,6 +319,7 @@ struct DevScene {
     int32_t n_mats;             // MatF records (distinct materials)
     int32_t n_xf;               // XformF records
     int32_t n_vn;               // triangles with vertex normals
+    uint32_t facts;             // FACT_* (materials and primitive kinds in use)
     // exact set
     const PrimD* prims_d;
     const XformD* xf_d;

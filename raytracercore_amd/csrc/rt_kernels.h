@@ -49,6 +49,25 @@ struct PathParams {
     const MatF* mats;
     const float4* vnormals;
     const PrimD* prims_d;       // the exact fp64 records by primitive ID (the vertex-normal re-hit test)
+    float4* ray_log;            // BVH kernels, instrumented launch only (rt_debug_ray_log): every finished
+    unsigned int* ray_log_n;    //   query as 3 float4 (o, prev | d | t, sg) appended at ray_log_n, up to
+    unsigned int ray_log_cap;   //   ray_log_cap records
+};
+
+// Trace-only kernel over a ray list (rt_debug_trace_rays): the wide BVH's speculative traversal
+// without the shading phase, for measuring what a wavefront split's traversal stage would take.
+struct TraceRaysParams {
+    const float4* rays;         // 3 float4 per ray as the ray log writes them
+    float2* hits;               // (t, bitcast sg) per ray
+    unsigned int n;
+    unsigned int* counter;      // ray dispenser (zeroed before the launch)
+    int* stack_ovf;
+    const TestRec* tests;
+    const Node4Q* nodes4;
+    const XformF* xf;
+    int root4;
+    int spec;                   // blocked lanes that trigger a leaf step (as PathParams.spec)
+    unsigned long long* stats;  // optional [3]: node visits, leaf-step lane slots, lane slots in all
 };
 
 #ifndef __HIPCC_RTC__ // host-side launch interface (not part of a hiprtc-compiled kernel)
@@ -73,6 +92,10 @@ size_t path_dyn_lds(const DevScene& s, int variant); // all dynamic LDS of a var
 hipError_t launch_path(const DevScene& s, const CameraF* d_cam, const PathParams* d_params, int variant,
                        int grid_blocks, hipStream_t stream, bool stats);
 int path_blocks_per_cu(int variant, size_t dyn_lds, bool stats, bool vn); // vn: scene has vertex-normal triangles
+// The trace-only kernel (waves per SIMD 6 / 7 / 8 with LDS stacks of 20 / 16 / 16 entries): blocks
+// per CU and launch (grid blocks of 256).
+int trace_rays_blocks_per_cu(int waves);
+hipError_t launch_trace_rays(const TraceRaysParams& p, int waves, int grid_blocks, hipStream_t stream);
 
 // partial -> fp64 planar accumulators (d_sum planes R | G | B, each `plane` doubles apart;
 // 0 = w*h), d_samples, d_misses (row-major w*h), added to.

@@ -192,6 +192,9 @@ struct rt_scene {
     DevBuf<uint32_t> samples, misses;
     DevBuf<int32_t> ids;
     bool stats_on = false;      // launch the instrumented kernel (rt_scene_set_stats)
+    float4* ray_log = nullptr;  // rt_debug_ray_log (instrumented BVH launches)
+    unsigned int* ray_log_n = nullptr;
+    unsigned int ray_log_cap = 0;
     int stats_blocks_per_cu = 1;
     DevBuf<unsigned long long> stats_buf;
     CameraD camd{};
@@ -912,6 +915,14 @@ int upload_scene(rt_scene* s)
         }
         mat_of[i] = it->second;
     }
+    uint32_t facts = 0;
+    for (const HostPrim& p : H) {
+        if (std::isinf(p.shininess) && p.shininess > 0) facts |= FACT_INF_SHININESS;
+        if ((float)p.ior != 0.0f) facts |= FACT_IOR;
+        if (p.flags & (F_TRANSFORMED | F_HASNORMALS)) facts |= FACT_XF_VN;
+        if (p.kind == RT_PRIM_SPHERE) facts |= FACT_SPHERE;
+    }
+    if (getenv("RTCORE_NO_FACTS")) facts = FACT_ALL; // A/B: every shading feature compiled in
     auto set_mats = [&](std::vector<PrimF>& v) { // PrimF.d.w = the material of the record's ID
         for (PrimF& f : v) {
             int32_t id;
@@ -1077,6 +1088,7 @@ int upload_scene(rt_scene* s)
     d.vnormals = s->vnormals.p;
     d.n_mats = (int)mats.size();
     d.n_xf = (int)xf.size();
+    d.facts = facts;
     d.n_vn = 0;
     for (const HostPrim& p : H) d.n_vn += (p.kind == RT_PRIM_TRIANGLE && (p.flags & F_HASNORMALS)) ? 1 : 0;
     d.prims_d = s->prims_d.p;
@@ -1379,6 +1391,9 @@ int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t
     p.counter = s->counter.p;
     p.rays = d_rays;
     p.stats = s->stats_on ? s->stats_buf.p : nullptr;
+    p.ray_log = s->stats_on ? s->ray_log : nullptr;
+    p.ray_log_n = s->ray_log_n;
+    p.ray_log_cap = s->ray_log_cap;
     // order after the previous operation when it ran on another stream (shared scratch)
     if (s->any_op && stream != s->last_stream) HIP_TRY(hipStreamWaitEvent(stream, s->done_ev, 0));
     HIP_TRY(hipMemsetAsync(p.counter, 0, sizeof(unsigned int), stream));
@@ -1597,6 +1612,61 @@ int rt_set_jit(int32_t on)
         return RT_ERR_ARG;
     }
     jit_set_enabled(on == 1);
+    return RT_OK;
+}
+
+int rt_debug_ray_log(rt_scene* s, void* d_log, uint32_t cap, void* d_count)
+{
+    if (!s || (d_log && !d_count)) {
+        set_error("rt_debug_ray_log: bad argument");
+        return RT_ERR_ARG;
+    }
+    s->ray_log = static_cast<float4*>(d_log);
+    s->ray_log_n = static_cast<unsigned int*>(d_count);
+    s->ray_log_cap = d_log ? cap : 0;
+    return RT_OK;
+}
+
+int rt_debug_trace_rays(rt_scene* s, const void* d_rays, uint32_t n, void* d_hits, int32_t waves, void* d_stats,
+                        void* stream, float* ms)
+{
+    if (!s || !d_rays || !d_hits || !ms || waves < 6 || waves > 8) {
+        set_error("rt_debug_trace_rays: bad argument");
+        return RT_ERR_ARG;
+    }
+    if (s->dev.n_pln > 0 || s->bvh.n_nodes4 == 0) {
+        set_error("rt_debug_trace_rays: needs a wide BVH and a scene without planes");
+        return RT_ERR_STATE;
+    }
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int grid = s->n_cu * trace_rays_blocks_per_cu(waves);
+    HIP_TRY(s->stack_ovf.reserve((size_t)grid * 256 * kStackOverflow));
+    HIP_TRY(s->counter.reserve(1));
+    HIP_TRY(hipMemsetAsync(s->counter.p, 0, sizeof(unsigned int), st));
+    TraceRaysParams p{};
+    p.rays = static_cast<const float4*>(d_rays);
+    p.hits = static_cast<float2*>(d_hits);
+    p.n = n;
+    p.counter = s->counter.p;
+    p.stack_ovf = s->stack_ovf.p;
+    p.tests = s->dev.tests_bvh;
+    p.nodes4 = s->dev.nodes4;
+    p.xf = s->dev.xf;
+    p.root4 = s->dev.root4;
+    p.spec = 16;
+    if (const char* e = getenv("RTCORE_BVH_SPEC")) p.spec = std::max(1, std::min(64, atoi(e)));
+    p.stats = static_cast<unsigned long long*>(d_stats);
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, st));
+    HIP_TRY(launch_trace_rays(p, waves, grid, st));
+    HIP_TRY(hipEventRecord(e1, st));
+    HIP_TRY(hipEventSynchronize(e1));
+    HIP_TRY(hipEventElapsedTime(ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     return RT_OK;
 }
 

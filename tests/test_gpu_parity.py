@@ -882,3 +882,44 @@ def test_scene_specialised_cache_untrusted_dir_is_not_used(tmp_path):
     assert r["status"] == 1.0 and stat.S_IMODE(os.stat(fresh).st_mode) == 0o700
     assert len([f for f in os.listdir(fresh) if f.endswith(".co")]) == 1
     assert _cache_probe(fresh, 3)["cached"] == 1.0
+
+
+def test_trace_only_kernel_reproduces_logged_hits(rc):
+    """rt_debug_ray_log + rt_debug_trace_rays (the wavefront-split measurement): the
+    instrumented wide-BVH kernel logs every finished query of a small mesh render, and the
+    trace-only kernel re-traces them at 6, 7 and 8 waves per SIMD with bit-identical closest hits."""
+    import torch
+
+    from raytracercore_amd.scenes import mesh_scene_text
+
+    W, H, spp = 96, 64, 4
+    scene = rc.SceneLoader.from_text(mesh_scene_text(nx=41, ny=41))
+    gpu = rc.GpuRaytracer(scene, 0, size=(W, H), traversal=rc.RT_TRAVERSAL_BVH)
+    dev = torch.device("cuda", 0)
+    cap = W * H * spp * 12
+    log = torch.zeros(cap * 12, dtype=torch.float32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    lib = gpu.lib
+    assert lib.rt_debug_ray_log(gpu.handle, C.c_void_p(log.data_ptr()), cap, C.c_void_p(cnt.data_ptr())) == 0
+    gpu.set_stats(True)
+    s, n_, m, rays = gpu.render_tile(0, 0, W, H, spp, seed=3)
+    gpu.set_stats(False)
+    assert lib.rt_debug_ray_log(gpu.handle, None, 0, None) == 0
+    n = int(cnt.item())
+    assert n == rays > W * H * spp
+    logged = log[: n * 12].view(n, 3, 4)
+    assert int((logged[:, 2, 1].view(torch.int32) >= 0).sum()) > 0.5 * n  # most queries meet the room or the field
+    for waves in (6, 7, 8):
+        hits = torch.full((n, 2), -7.0, dtype=torch.float32, device=dev)
+        ms = C.c_float(0)
+        stats = torch.zeros(3, dtype=torch.int64, device=dev)
+        assert lib.rt_debug_trace_rays(gpu.handle, C.c_void_p(log.data_ptr()), n, C.c_void_p(hits.data_ptr()), waves,
+                                       C.c_void_p(stats.data_ptr()), None, C.byref(ms)) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(hits[:, 0], logged[:, 2, 0])
+        assert torch.equal(hits[:, 1].view(torch.int32), logged[:, 2, 1].view(torch.int32))
+        assert ms.value > 0 and int(stats[2].item()) >= int(stats[0].item()) + int(stats[1].item()) > 0
+    with pytest.raises(rc.RtError):
+        rc._check(lib.rt_debug_trace_rays(gpu.handle, C.c_void_p(log.data_ptr()), n, C.c_void_p(hits.data_ptr()), 5,
+                                          None, None, C.byref(ms)))
+    gpu.close()

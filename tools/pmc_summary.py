@@ -51,5 +51,13 @@ if json_out and "FETCH_SIZE" in tot and "WRITE_SIZE" in tot:
     rec = {"fetch_size_kb": tot["FETCH_SIZE"], "write_size_kb": tot["WRITE_SIZE"],
            "traffic_bytes": 2 * tot["FETCH_SIZE"] * 1024 + tot["WRITE_SIZE"] * 1024,
            "note": "per path-kernel launch; FETCH_SIZE doubled per the gfx950 correction", "source": d}
+    # the compute view's hardware figures (bench.py roofline.counter_view): FP32 FLOP counter per
+    # launch (x 64 lanes per wave-level count), VALU issue rate and lane utilisation
+    if "SQ_INSTS_VALU_FLOPS_FP32" in tot:
+        rec["valu_flops_fp32"] = tot["SQ_INSTS_VALU_FLOPS_FP32"]
+    if "GRBM_GUI_ACTIVE" in tot and "SQ_INSTS_VALU" in tot:
+        rec["valu_issue_per_simd_cycle"] = round(tot["SQ_INSTS_VALU"] / 1024 / (tot["GRBM_GUI_ACTIVE"] / 8), 4)
+    if "SQ_THREAD_CYCLES_VALU" in tot and "SQ_ACTIVE_INST_VALU" in tot:
+        rec["valu_lane_utilisation"] = round(tot["SQ_THREAD_CYCLES_VALU"] / (64 * tot["SQ_ACTIVE_INST_VALU"]), 4)
     json.dump(rec, open(json_out, "w"), indent=1)
     print("wrote", json_out, rec["traffic_bytes"])
