@@ -20,8 +20,12 @@ for f in glob.glob(os.path.join(d, "pmc*", "pmc_counter_collection.csv")):
         kname = r["Kernel_Name"]
         i = kname.find("path_kernel")
         tmpl = kname[i:].split(">")[0] if i >= 0 else ""
+        # template arguments: path_kernel<CULL, LDS, STATS, VN>, path_kernel_bvh<WIDTH, STACK, LDS, STATS, VN>
+        targs = [a.strip() for a in tmpl.split("<", 1)[1].split(",")] if "<" in tmpl else []
+        stats_arg = targs[3] if tmpl.startswith("path_kernel_bvh") and len(targs) > 3 else \
+            (targs[2] if len(targs) > 2 else "false")
         hit = (sub in kname) if sub else any(k in kname for k in PATH_KERNELS)
-        if hit and not tmpl.endswith("true"):  # skip the instrumented (STATS) variant
+        if hit and stats_arg != "true":  # skip the instrumented (STATS) variant and probes
             key = (os.path.basename(os.path.dirname(f)), int(r["Dispatch_Id"]))
             agg[key][r["Counter_Name"]] += float(r["Counter_Value"])
             names[key] = r["Kernel_Name"][:70]
