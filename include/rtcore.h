@@ -227,6 +227,13 @@ int rt_debug_brute_layout(const rt_prim* prims, int32_t n_prims, int32_t* out, i
    counters to d_stats[3] (node-step lane slots, leaf-step lane slots, lane slots in all) and the
    kernel's time (hipEvents) to *ms.  BVH traversal modes of a scene without planes only. */
 int rt_debug_ray_log(rt_scene* scene, void* d_log, uint32_t cap, void* d_count);
+/* Host only: the kernels' vertex-normal re-hit test -- Triangle.RayTraceAVXFaster in
+   fp64 on the ray that leaves the triangle (v0, e01, e02) from its point fma(e01, u, fma(e02, v, v0))
+   along dir (fp32, as the kernel holds it).  Returns 1 if that query meets the triangle again, 0 if
+   not (negative rt_status on bad arguments); *inside = its Inside flag, *t its distance, origin[3]
+   the start point used. */
+int rt_debug_vn_rehit(const double* v0, const double* e01, const double* e02, int32_t mirror, double u, double v,
+                      const float* dir, int32_t* inside, double* t, double* origin);
 int rt_debug_trace_rays(rt_scene* scene, const void* d_rays, uint32_t n, void* d_hits, int32_t waves_per_simd,
                         void* d_stats, void* stream, float* ms);
 

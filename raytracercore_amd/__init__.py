@@ -167,6 +167,8 @@ def load_library(path: str = "") -> C.CDLL:
         "rt_ref_bvh_export": (C.c_int, [P(rt_prim), C.c_int32, P(C.c_int32), P(C.c_double), P(C.c_int32),
                                         P(C.c_int32)]),
         "rt_debug_ray_log": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
+        "rt_debug_vn_rehit": (C.c_int, [P(C.c_double), P(C.c_double), P(C.c_double), C.c_int32, C.c_double,
+                                        C.c_double, P(C.c_float), P(C.c_int32), P(C.c_double), P(C.c_double)]),
         "rt_debug_trace_rays": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_int32, C.c_void_p,
                                           C.c_void_p, P(C.c_float)]),
     }

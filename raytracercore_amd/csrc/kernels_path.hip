@@ -557,7 +557,8 @@ __device__ __forceinline__ float one_minus_exp2_2a(float a)
 // normal and the geometric side agree); a smooth normal (Triangle.GetNormal, :209-224) can send the
 // ray under the geometric surface, and then it is not.  The kernel evaluates the same fp64
 // expression on its own hit point.
-__device__ __noinline__ bool vn_rehit_test(const PrimD& P, double u, double v, V3 dir, bool& inside)
+__host__ __device__ __noinline__ bool vn_rehit_test(const PrimD& P, double u, double v, V3 dir, bool& inside,
+                                                   double* t_out = nullptr, double* o_out = nullptr)
 {
     const Vec4d a = P.a, e1 = P.b, e2 = P.c;
     const double d[4] = {(double)dir.x, (double)dir.y, (double)dir.z, 0.0};
@@ -582,6 +583,12 @@ __device__ __noinline__ bool vn_rehit_test(const PrimD& P, double u, double v, V
     bool rej = (u2 < 0) | (v2 < 0) | (t2 < 0);
     rej |= (P.flags & F_MIRROR) ? ((u2 > 1) | (v2 > 1)) : ((u2 + v2) > 1);
     inside = invz < 0;
+    if (t_out) *t_out = t2;
+    if (o_out) {
+        o_out[0] = o[0];
+        o_out[1] = o[1];
+        o_out[2] = o[2];
+    }
     return !rej;
 }
 
@@ -1620,6 +1627,20 @@ PathScene make_path_scene(const DevScene& s)
 
 #ifndef __HIPCC_RTC__
 int path_wide_stack() { return RT_WIDE_STACK; }
+
+int debug_vn_rehit(const double v0[3], const double e01[3], const double e02[3], int mirror, double u, double v,
+                   const float dir[3], int* inside, double* t, double o[3])
+{
+    PrimD P{};
+    P.a = Vec4d{v0[0], v0[1], v0[2], 1.0};
+    P.b = Vec4d{e01[0], e01[1], e01[2], 0.0};
+    P.c = Vec4d{e02[0], e02[1], e02[2], 0.0};
+    P.flags = mirror ? F_MIRROR : 0u;
+    bool in = false;
+    const bool hit = vn_rehit_test(P, u, v, V3{dir[0], dir[1], dir[2]}, in, t, o);
+    *inside = in ? 1 : 0;
+    return hit ? 1 : 0;
+}
 
 size_t path_lds_bytes(const DevScene& s)
 {

@@ -95,6 +95,11 @@ int path_blocks_per_cu(int variant, size_t dyn_lds, bool stats, bool vn); // vn:
 // The trace-only kernel (waves per SIMD 6 / 7 / 8 with LDS stacks of 20 / 16 / 16 entries): blocks
 // per CU and launch (grid blocks of 256).
 int trace_rays_blocks_per_cu(int waves);
+// Host evaluation of the kernels' vertex-normal re-hit test (vn_rehit_test): Triangle.RayTraceAVXFaster
+// in fp64 from the hit point fma(e01, u, fma(e02, v, v0)) along dir; returns 1 on a hit, with its
+// Inside flag, t and the origin used.
+int debug_vn_rehit(const double v0[3], const double e01[3], const double e02[3], int mirror, double u, double v,
+                   const float dir[3], int* inside, double* t, double o[3]);
 hipError_t launch_trace_rays(const TraceRaysParams& p, int waves, int grid_blocks, hipStream_t stream);
 
 // partial -> fp64 planar accumulators (d_sum planes R | G | B, each `plane` doubles apart;

@@ -1615,6 +1615,19 @@ int rt_set_jit(int32_t on)
     return RT_OK;
 }
 
+int rt_debug_vn_rehit(const double* v0, const double* e01, const double* e02, int32_t mirror, double u, double v,
+                      const float* dir, int32_t* inside, double* t, double* origin)
+{
+    if (!v0 || !e01 || !e02 || !dir || !inside || !t || !origin) {
+        set_error("rt_debug_vn_rehit: bad argument");
+        return RT_ERR_ARG;
+    }
+    int in = 0;
+    const int hit = debug_vn_rehit(v0, e01, e02, mirror, u, v, dir, &in, t, origin);
+    *inside = in;
+    return hit;
+}
+
 int rt_debug_ray_log(rt_scene* s, void* d_log, uint32_t cap, void* d_count)
 {
     if (!s || (d_log && !d_count)) {
