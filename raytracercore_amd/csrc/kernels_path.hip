@@ -189,11 +189,6 @@ __device__ __forceinline__ void rect_group(RectP r, int n, V3 o, V3 d, V3 id, V3
 // face the ray leaves (self-hit).  The entry wins when both are hits.  Equivalent to testing the
 // six faces as rectangles (a convex box is met at most twice), up to ties on its edges.
 // SUB: oi holds o itself (frame-local rays), as in hit_rect.
-#ifdef RT_EXP_NO_KEEP_FOLD // A/B switch: test the keep bit even when every face keeps
-#define RT_KEEP_ALL(keep, mask) false
-#else
-#define RT_KEEP_ALL(keep, mask) (((keep) & (mask)) == (mask))
-#endif
 template <bool SUB>
 __device__ __forceinline__ void hit_box(const BoxRec& B, V3 o, V3 d, V3 id, V3 oi, int prev, Best& b)
 {
@@ -216,15 +211,15 @@ __device__ __forceinline__ void hit_box(const BoxRec& B, V3 o, V3 d, V3 id, V3 o
     int fe = 0, fo = 0;
     if (keep & 0x3Fu) { // some face keeps entry hits (wave-uniform)
         fe = te == nx ? sx : (te == ny ? 2 + sy : 4 + sz);
-        // the keep bit is tested unless every face keeps (a constant in a scene-specialised build;
-        // selecting on it at run time cost more than the test)
+        // the keep bit is tested unconditionally: selecting on "every face keeps" cost more, and
+        // folding that case in the scene-specialised build measured no change (round 3)
         ok_e = meet & (__float_as_uint(te) < __float_as_uint(b.t)) & (((perm >> (4 * fe)) & 15u) != rel_prev) &
-               (RT_KEEP_ALL(keep, 0x3Fu) || ((keep >> fe) & 1u) != 0);
+               (((keep >> fe) & 1u) != 0);
     }
     if (keep & 0x3F00u) { // some face keeps exit hits
         fo = tx == fx ? 1 - sx : (tx == fy ? 3 - sy : 5 - sz);
         ok_x = meet & (__float_as_uint(tx) < __float_as_uint(b.t)) & (((perm >> (4 * fo)) & 15u) != rel_prev) &
-               (RT_KEEP_ALL(keep, 0x3F00u) || ((keep >> (8 + fo)) & 1u) != 0);
+               (((keep >> (8 + fo)) & 1u) != 0);
     }
     const bool ok = ok_e | ok_x;
     b.t = ok ? (ok_e ? te : tx) : b.t;
