@@ -218,7 +218,8 @@ int rt_scene_check_bvh(rt_scene* scene);
 #define RT_LAYOUT_COUNT 10
 int rt_debug_brute_layout(const rt_prim* prims, int32_t n_prims, int32_t* out, int32_t n_out);
 /* Measurement of a wavefront split's traversal stage.  rt_debug_ray_log: while
-   the instrumented kernel runs (rt_scene_set_stats), the BVH kernels append every finished query
+   the next instrumented launch of a BVH kernel runs (rt_scene_set_stats; one launch only, then
+   logging is off again), the kernel appends every finished query
    to d_log as 3 float4 (origin, previous primitive ID | direction, frame pixel index | closest t,
    hit slot, bounce) at the
    device counter *d_count, up to cap records (d_log = NULL turns logging off).

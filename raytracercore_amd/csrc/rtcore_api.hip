@@ -1391,9 +1391,12 @@ int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t
     p.counter = s->counter.p;
     p.rays = d_rays;
     p.stats = s->stats_on ? s->stats_buf.p : nullptr;
-    p.ray_log = s->stats_on ? s->ray_log : nullptr;
+    // rt_debug_ray_log arms the next instrumented BVH launch only, so a buffer the caller frees
+    // afterwards is never written
+    p.ray_log = (s->stats_on && s->variant >= 4) ? s->ray_log : nullptr;
     p.ray_log_n = s->ray_log_n;
     p.ray_log_cap = s->ray_log_cap;
+    if (p.ray_log) s->ray_log = nullptr;
     // order after the previous operation when it ran on another stream (shared scratch)
     if (s->any_op && stream != s->last_stream) HIP_TRY(hipStreamWaitEvent(stream, s->done_ev, 0));
     HIP_TRY(hipMemsetAsync(p.counter, 0, sizeof(unsigned int), stream));

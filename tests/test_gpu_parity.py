@@ -903,9 +903,10 @@ def test_trace_only_kernel_reproduces_logged_hits(rc):
     assert lib.rt_debug_ray_log(gpu.handle, C.c_void_p(log.data_ptr()), cap, C.c_void_p(cnt.data_ptr())) == 0
     gpu.set_stats(True)
     s, n_, m, rays = gpu.render_tile(0, 0, W, H, spp, seed=3)
-    gpu.set_stats(False)
-    assert lib.rt_debug_ray_log(gpu.handle, None, 0, None) == 0
     n = int(cnt.item())
+    gpu.render_tile(0, 0, W, H, spp, seed=4)  # logging armed one launch only: nothing more is written
+    gpu.set_stats(False)
+    assert int(cnt.item()) == n
     assert n == rays > W * H * spp
     logged = log[: n * 12].view(n, 3, 4)
     assert int((logged[:, 2, 1].view(torch.int32) >= 0).sum()) > 0.5 * n  # most queries meet the room or the field
