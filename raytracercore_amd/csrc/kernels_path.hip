@@ -39,13 +39,29 @@ __device__ __forceinline__ V3 operator*(V3 a, float s) { return {a.x * s, a.y * 
 __device__ __forceinline__ V3 operator*(V3 a, V3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
 __device__ __forceinline__ V3 operator-(V3 a) { return {-a.x, -a.y, -a.z}; }
 __device__ __forceinline__ float dot(V3 a, V3 b) { return fmaf(a.x, b.x, fmaf(a.y, b.y, a.z * b.z)); }
-__device__ __forceinline__ float dot4(float4 r, V3 p) { return fmaf(r.x, p.x, fmaf(r.y, p.y, fmaf(r.z, p.z, r.w))); }
-__device__ __forceinline__ float dot3(float4 r, V3 p) { return fmaf(r.x, p.x, fmaf(r.y, p.y, r.z * p.z)); }
+// Products with a scene or camera field.  In the scene-specialised build those fields are literals,
+// and IEEE rules keep fmaf(0, x, y) as an instruction (x could be infinite, and y + 0 is not y for
+// y = -0): axis-aligned cameras, rotation frames and two-sided rectangles carried ~20 such terms per
+// query on bounce.txt.  A term whose literal factor is zero is dropped there; the generic kernel
+// computes the same values except for the sign of an exact zero (x is always finite here).
+__device__ __forceinline__ bool known_zero(float c)
+{
+#if defined(RT_SCENE_CONST) && !defined(RT_EXP_NO_KFOLD)
+    return __builtin_constant_p(c) && c == 0.0f;
+#else
+    (void)c;
+    return false;
+#endif
+}
+__device__ __forceinline__ float kfma(float a, float b, float c) { return (known_zero(a) || known_zero(b)) ? c : fmaf(a, b, c); }
+__device__ __forceinline__ float kmul(float a, float b) { return (known_zero(a) || known_zero(b)) ? -0.0f : a * b; }
+__device__ __forceinline__ float dot4(float4 r, V3 p) { return kfma(r.x, p.x, kfma(r.y, p.y, kfma(r.z, p.z, r.w))); }
+__device__ __forceinline__ float dot3(float4 r, V3 p) { return kfma(r.x, p.x, kfma(r.y, p.y, kmul(r.z, p.z))); }
 __device__ __forceinline__ V3 cross(V3 a, V3 b)
 {
     return {fmaf(a.y, b.z, -a.z * b.y), fmaf(a.z, b.x, -a.x * b.z), fmaf(a.x, b.y, -a.y * b.x)};
 }
-__device__ __forceinline__ V3 madd(V3 a, float s, V3 c) { return {fmaf(a.x, s, c.x), fmaf(a.y, s, c.y), fmaf(a.z, s, c.z)}; }
+__device__ __forceinline__ V3 madd(V3 a, float s, V3 c) { return {kfma(a.x, s, c.x), kfma(a.y, s, c.y), kfma(a.z, s, c.z)}; }
 __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 __device__ __forceinline__ V3 normalize(V3 a) { return a * __builtin_amdgcn_rsqf(dot(a, a)); }
@@ -149,7 +165,7 @@ __device__ __forceinline__ void hit_rect(const RectRec& R, int sg, V3 o, V3 d, V
     const bool in2 = fabsf(fmaf(t, d2, o2) - R.m2) <= R.h2;
     // 0 <= t < best as one unsigned compare of the bit patterns (b.t >= 0; NaN and -t fail)
     const bool near = __float_as_uint(t) < __float_as_uint(b.t);
-    const bool ok = near & in1 & in2 & (R.cull * da <= 0.0f) & (R.id != prev);
+    const bool ok = near & in1 & in2 & (kmul(R.cull, da) <= 0.0f) & (R.id != prev);
     b.t = ok ? t : b.t; // the shading step rebuilds the hit point from t
     b.sg = ok ? sg : b.sg;
 }
