@@ -370,24 +370,38 @@ __device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb)
 // Per-lane traversal stack: the first STACK entries in LDS (stride 256 = the block's lanes), deeper
 // entries in a global overflow area (stride = all lanes of the grid), reached only by rare deep
 // paths; the host bounds the depth any ray can need by STACK + RT_STACK_OVF.
+// The two parts are typed by address space: with plain pointers the compiler merged the LDS and the
+// overflow access of push / pop into one flat access through a selected pointer (a flat store or
+// load, plus the pointer arithmetic, on every push and pop, and through the texture addresser).
+// The bases are wave-uniform and the lane's offset is formed at use: per-lane pointers held across
+// the loop were spilled to scratch and reloaded at every push (C4 52.4 -> 66.6 ms).
 #define RT_STACK_OVF 40
+typedef __attribute__((address_space(3))) int LdsInt;
+typedef __attribute__((address_space(1))) int GlobalInt;
 struct TravStack {
-    int* lds;
-    int* ovf;
-    int ovf_stride;
+    LdsInt* lds;    // the block's stack array (entry e of thread t at e * 256 + t)
+    GlobalInt* ovf; // the grid's overflow area (entry e of global thread g at e * grid threads + g)
 };
+__device__ __forceinline__ TravStack make_stack(int* lds_base, int* ovf_base)
+{
+    return TravStack{(LdsInt*)lds_base, (GlobalInt*)ovf_base};
+}
+__device__ __forceinline__ unsigned ovf_slot(int e)
+{
+    return (unsigned)e * (gridDim.x * 256u) + blockIdx.x * 256u + threadIdx.x;
+}
 template <int STACK>
 __device__ __forceinline__ void push(const TravStack& st, int& sp, int v)
 {
-    if (sp < STACK) st.lds[sp * 256] = v;
-    else st.ovf[(sp - STACK) * st.ovf_stride] = v;
+    if (sp < STACK) st.lds[sp * 256 + (int)threadIdx.x] = v;
+    else st.ovf[ovf_slot(sp - STACK)] = v;
     sp++;
 }
 template <int STACK>
 __device__ __forceinline__ int pop_ref(const TravStack& st, int& sp)
 {
     --sp;
-    return sp < STACK ? st.lds[sp * 256] : st.ovf[(sp - STACK) * st.ovf_stride];
+    return sp < STACK ? st.lds[sp * 256 + (int)threadIdx.x] : st.ovf[ovf_slot(sp - STACK)];
 }
 
 template <int STACK>
@@ -416,8 +430,8 @@ __device__ __forceinline__ void wide_visit(const Node4Q& q, V3 id, V3 oi, float 
                                        fmaf(ubyte(nz, K), az, bz)), 0.0f);                                         \
         const float tmax = fminf(fminf(fmaf(ubyte(fx, K), ax, bx), fmaf(ubyte(fy, K), ay, by)),                   \
                                  fmaf(ubyte(fz, K), az, bz));                                                      \
-        D = (K < nc && tmin <= fminf(tmax * 1.00000024f, tmax_best)) ? tmin : __builtin_huge_valf();             \
-    }
+        D = ((K < nc) & (tmin <= fminf(tmax * 1.00000024f, tmax_best))) ? tmin : __builtin_huge_valf();         \
+    } // (K < nc) without short-circuit: "&&" made each child a divergent branch
     RT_WIDE_CHILD(0, d0)
     RT_WIDE_CHILD(1, d1)
     RT_WIDE_CHILD(2, d2)
@@ -1143,7 +1157,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
     const ParamsC& P0 = *(const ParamsC*)pp;
     __shared__ int stack_mem[STACK * 256];
     extern __shared__ float4 lds_scene[];
-    const TravStack stk{stack_mem + threadIdx.x, P0.stack_ovf + blockIdx.x * 256 + threadIdx.x, (int)gridDim.x * 256};
+    const TravStack stk = make_stack(stack_mem, P0.stack_ovf);
     const ShadeRecs R = stage_scene<LDS>(P0.scene, P0.prims, P0.mats, P0.xf, lds_scene);
     // hot wide nodes after the staged shading records (dynamic LDS; see path_lds_bytes)
     Node4Q* lds_hot = reinterpret_cast<Node4Q*>(lds_scene + (LDS ? scene_lds_float4s(P0.scene) : 0));
@@ -1379,7 +1393,7 @@ template <int STACK, int WAVES, bool STATS>
 __global__ void __launch_bounds__(256, WAVES) trace_rays_kernel(TraceRaysParams p)
 {
     __shared__ int stack_mem[STACK * 256];
-    const TravStack stk{stack_mem + threadIdx.x, p.stack_ovf + blockIdx.x * 256 + threadIdx.x, (int)gridDim.x * 256};
+    const TravStack stk = make_stack(stack_mem, p.stack_ovf);
     const int lane = threadIdx.x & 63;
     const RT_AS_CONST TestRec* tests = (const RT_AS_CONST TestRec*)p.tests;
     const RT_AS_CONST Node4Q* nodes4 = (const RT_AS_CONST Node4Q*)p.nodes4;
