@@ -404,6 +404,16 @@ __device__ __forceinline__ int pop_ref(const TravStack& st, int& sp)
     return sp < STACK ? st.lds[sp * 256 + (int)threadIdx.x] : st.ovf[ovf_slot(sp - STACK)];
 }
 
+__device__ __forceinline__ void pin_rec(TestRec& t)
+{
+    typedef float F4 __attribute__((ext_vector_type(4)));
+    float4* f = &t.r0;
+    for (int q = 0; q < 4; q++) {
+        F4 v = {f[q].x, f[q].y, f[q].z, f[q].w};
+        asm volatile("" : "+v"(v));
+        f[q] = make_float4(v.x, v.y, v.z, v.w);
+    }
+}
 template <int STACK>
 __device__ __forceinline__ void wide_visit(const Node4Q& q, V3 id, V3 oi, float best, int& ref, int& sp,
                                            const TravStack& stk, bool& pop)
@@ -1258,6 +1268,12 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                     TestRec r[RT_SPEC_PRIMS];
 #pragma unroll
                     for (int j = 0; j < RT_SPEC_PRIMS; j++) r[j] = tests[k + j]; // kTestSpares zero records follow the last leaf
+                    // all rows in registers before the kind dispatch: otherwise the compiler sinks
+                    // row loads into the triangle / sphere branches, one more round trip per step
+                    // (C4 49.9 -> 48.9 ms; fetching the second record only when the leaf has one, by
+                    // an out-of-range buffer offset, measured no further change)
+#pragma unroll
+                    for (int j = 0; j < RT_SPEC_PRIMS; j++) pin_rec(r[j]);
 #pragma unroll
                     for (int j = 0; j < RT_SPEC_PRIMS; j++) {
                         if (j == 0 || k + j < kend) {
@@ -1461,6 +1477,8 @@ __global__ void __launch_bounds__(256, WAVES) trace_rays_kernel(TraceRaysParams 
                     TestRec r[RT_SPEC_PRIMS];
 #pragma unroll
                     for (int j = 0; j < RT_SPEC_PRIMS; j++) r[j] = tests[k + j];
+#pragma unroll
+                    for (int j = 0; j < RT_SPEC_PRIMS; j++) pin_rec(r[j]);
 #pragma unroll
                     for (int j = 0; j < RT_SPEC_PRIMS; j++)
                         if (j == 0 || k + j < kend) hit_any(r[j], k + j, o, d, prev, xf, b);
