@@ -404,15 +404,19 @@ __device__ __forceinline__ int pop_ref(const TravStack& st, int& sp)
     return sp < STACK ? st.lds[sp * 256 + (int)threadIdx.x] : st.ovf[ovf_slot(sp - STACK)];
 }
 
-__device__ __forceinline__ void pin_rec(TestRec& t)
+__device__ __forceinline__ void pin4(float4& f)
 {
     typedef float F4 __attribute__((ext_vector_type(4)));
-    float4* f = &t.r0;
-    for (int q = 0; q < 4; q++) {
-        F4 v = {f[q].x, f[q].y, f[q].z, f[q].w};
-        asm volatile("" : "+v"(v));
-        f[q] = make_float4(v.x, v.y, v.z, v.w);
-    }
+    F4 v = {f.x, f.y, f.z, f.w};
+    asm volatile("" : "+v"(v));
+    f = make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void pin_rec(TestRec& t)
+{
+    pin4(t.r0);
+    pin4(t.r1);
+    pin4(t.r2);
+    pin4(t.meta);
 }
 template <int STACK>
 __device__ __forceinline__ void wide_visit(const Node4Q& q, V3 id, V3 oi, float best, int& ref, int& sp,
@@ -638,7 +642,7 @@ __device__ __forceinline__ Best query_start(const SceneT& s, int prev)
 
 // One bounce of Raytracer.GetColor after the closest-hit query.  Returns 0 to continue the
 // path, 1 if the sample ended with colour `col`, 2 if it ended as a miss (Placeholder).
-template <bool VN, class SceneT, class VnP, class TestP>
+template <bool VN, bool PIN = false, class SceneT, class VnP, class TestP>
 __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ prims, const MatF* __restrict__ mats,
                                      const XformF* __restrict__ xfs, VnP vnormals, TestP tests, const PrimD* prims_d,
                                      const Best& b, Sample& S, V3& col)
@@ -649,7 +653,12 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
         return 1;
     }
     bool gin = (b.sg & 1) != 0;
-    const PrimF P = prims[b.sg >> 1];
+    PrimF P = prims[b.sg >> 1];
+    if (PIN) { // records from global memory: every field in flight at once (see pin_rec)
+        pin4(P.a);
+        pin4(P.b);
+        pin4(P.d);
+    }
     const uint32_t fl = __float_as_uint(P.b.w);
     const int id = __float_as_int(P.a.w);
     const MatF& M = mats[__float_as_int(P.d.w)]; // the primitive's material (deduplicated table)
@@ -959,12 +968,12 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
 }
 
 // After a closest-hit query: one bounce of GetColor; a finished sample goes into the item's sums.
-template <bool VN, class SceneT, class VnP, class TestP>
+template <bool VN, bool PIN = false, class SceneT, class VnP, class TestP>
 __device__ __forceinline__ void bounce(Lane& L, Sample& S, const SceneT& s, const ShadeRecs& R, VnP vnormals, TestP tests,
                                        const PrimD* prims_d, const Best& b)
 {
     V3 col;
-    const int r = shade<VN>(s, R.prims, R.mats, R.xfs, vnormals, tests, prims_d, b, S, col);
+    const int r = shade<VN, PIN>(s, R.prims, R.mats, R.xfs, vnormals, tests, prims_d, b, S, col);
     if (r != 0) {
         const bool hit = r == 1;
         L.ar += hit ? col.x : 0.0f;
@@ -1224,7 +1233,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                         r[2] = make_float4(b.t, __int_as_float(b.sg), __int_as_float(S.bounce), 0.0f);
                     }
                 }
-                bounce<VN>(L, S, s, R, vnormals, tests, pq->prims_d, b);
+                bounce<VN, !LDS>(L, S, s, R, vnormals, tests, pq->prims_d, b);
                 done = false;
             }
             refill<true>(L, S, p, s, *cp, lane, total);
