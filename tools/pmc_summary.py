@@ -50,6 +50,15 @@ if "GRBM_GUI_ACTIVE" in tot and "SQ_INSTS_VALU" in tot:
           "select and min/max forms, tools/micro/valu_forms.hip)")
 if "SQ_THREAD_CYCLES_VALU" in tot and "SQ_ACTIVE_INST_VALU" in tot:
     print("VALU lane utilisation", tot["SQ_THREAD_CYCLES_VALU"] / (64 * tot["SQ_ACTIVE_INST_VALU"]))
+if "TA_BUSY_avr" in tot and "GRBM_GUI_ACTIVE" in tot:
+    # the vector-memory pipeline; TA_BUSY_avr is per CU, GRBM_GUI_ACTIVE summed over 8 XCDs
+    print("TA busy fraction", tot["TA_BUSY_avr"] / (tot["GRBM_GUI_ACTIVE"] / 8))
+if "TCP_TOTAL_CACHE_ACCESSES_sum" in tot and "TCP_TCC_READ_REQ_sum" in tot:
+    print("L1 (TCP) hit rate", 1 - tot["TCP_TCC_READ_REQ_sum"] / tot["TCP_TOTAL_CACHE_ACCESSES_sum"])
+if "TCP_TCC_READ_REQ_LATENCY_sum" in tot and tot.get("TCP_TCC_READ_REQ_sum"):
+    print("L1 -> L2 read latency (cycles)", tot["TCP_TCC_READ_REQ_LATENCY_sum"] / tot["TCP_TCC_READ_REQ_sum"])
+if "TCP_PENDING_STALL_CYCLES_sum" in tot and "GRBM_GUI_ACTIVE" in tot:
+    print("L1 pending-stall fraction", tot["TCP_PENDING_STALL_CYCLES_sum"] / 256 / (tot["GRBM_GUI_ACTIVE"] / 8))
 if json_out and "FETCH_SIZE" in tot and "WRITE_SIZE" in tot:
     # rocprofv3 reports kB; on gfx950 FETCH_SIZE counts half the bytes of wide reads (MI355X_MICROARCH.md, HBM)
     rec = {"fetch_size_kb": tot["FETCH_SIZE"], "write_size_kb": tot["WRITE_SIZE"],
