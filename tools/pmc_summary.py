@@ -55,7 +55,7 @@ if "TA_BUSY_avr" in tot and "GRBM_GUI_ACTIVE" in tot:
     print("TA busy fraction", tot["TA_BUSY_avr"] / (tot["GRBM_GUI_ACTIVE"] / 8))
 if "TCP_TOTAL_CACHE_ACCESSES_sum" in tot and "TCP_TCC_READ_REQ_sum" in tot:
     print("L1 (TCP) hit rate", 1 - tot["TCP_TCC_READ_REQ_sum"] / tot["TCP_TOTAL_CACHE_ACCESSES_sum"])
-if "TCP_TCC_READ_REQ_LATENCY_sum" in tot and tot.get("TCP_TCC_READ_REQ_sum"):
+if "TCP_TCC_READ_REQ_LATENCY_sum" in tot and tot.get("TCP_TCC_READ_REQ_sum", 0) > 1e7:  # (C2/C3: too few to average)
     print("L1 -> L2 read latency (cycles)", tot["TCP_TCC_READ_REQ_LATENCY_sum"] / tot["TCP_TCC_READ_REQ_sum"])
 if "TCP_PENDING_STALL_CYCLES_sum" in tot and "GRBM_GUI_ACTIVE" in tot:
     print("L1 pending-stall fraction", tot["TCP_PENDING_STALL_CYCLES_sum"] / 256 / (tot["GRBM_GUI_ACTIVE"] / 8))
