@@ -684,10 +684,10 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
     pos.z = axis == 3 ? P.a.z : pos.z;
     V3 n = sph ? (pos - xyz(P.a)) * P.b.y : xyz(P.d);
     float bu = 0.0f, bv = 0.0f; // vertex-normal triangle: the barycentrics of the hit
-    if ((s.facts & FACT_XF_VN) && (fl & (F_TRANSFORMED | F_HASNORMALS))) {
+    if ((s.facts & (FACT_XF | FACT_VN)) && (fl & (F_TRANSFORMED | F_HASNORMALS))) {
         if (sph) { // ellipsoid: the world normal is an affine map of the world hit point
             n = normalize(xf_point(xfs[__float_as_int(P.b.z)].normal, pos));
-        } else { // Triangle.GetNormal quirk: Normal is never set -> NaN when inside
+        } else if (s.facts & FACT_VN) { // Triangle.GetNormal quirk: Normal is never set -> NaN when inside
             const VnP vn = vnormals + 3 * id;
             const TestRec R = tests[b.sg >> 1]; // barycentrics (u, v) = rows 0, 1 of M (p, 1)
             bu = dot4(R.r0, pos);

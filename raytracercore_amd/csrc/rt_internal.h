@@ -36,9 +36,10 @@ enum : uint32_t {
 enum : uint32_t {
     FACT_INF_SHININESS = 1u << 0, // some material has Shininess = +inf (RandomShine draws no z)
     FACT_IOR = 1u << 1,           // some material has a RefractiveIndex (Fresnel / TIR)
-    FACT_XF_VN = 1u << 2,         // a transformed sphere or a vertex-normal triangle
+    FACT_XF = 1u << 2,            // a transformed sphere (ellipsoid normal)
     FACT_SPHERE = 1u << 3,        // some sphere
-    FACT_ALL = 0xFu,
+    FACT_VN = 1u << 4,            // a vertex-normal triangle (smooth normal, GetNormal's NaN quirk)
+    FACT_ALL = 0x1Fu,
 };
 
 // Axis-aligned rectangle (a Mirror parallelogram whose edges follow two coordinate axes, e.g.

@@ -919,7 +919,8 @@ int upload_scene(rt_scene* s)
     for (const HostPrim& p : H) {
         if (std::isinf(p.shininess) && p.shininess > 0) facts |= FACT_INF_SHININESS;
         if ((float)p.ior != 0.0f) facts |= FACT_IOR;
-        if (p.flags & (F_TRANSFORMED | F_HASNORMALS)) facts |= FACT_XF_VN;
+        if (p.flags & F_TRANSFORMED) facts |= FACT_XF;
+        if (p.flags & F_HASNORMALS) facts |= FACT_VN;
         if (p.kind == RT_PRIM_SPHERE) facts |= FACT_SPHERE;
     }
     if (getenv("RTCORE_NO_FACTS")) facts = FACT_ALL; // A/B: every shading feature compiled in
