@@ -851,6 +851,7 @@ struct Lane {
     float ar, ag, ab;
     unsigned cnt; // item bookkeeping: samples (bits 0-7) | misses (8-15) | samples left (16-31)
     unsigned pool_next, pool_end;
+    unsigned split_j; // lane 0: item ranges (after its own) this wave found spent (PathParams::n_split)
 };
 
 __device__ __forceinline__ void lane_init(Lane& L)
@@ -863,6 +864,7 @@ __device__ __forceinline__ void lane_init(Lane& L)
     L.ar = L.ag = L.ab = 0.0f;
     L.cnt = 0;
     L.pool_next = L.pool_end = 0;
+    L.split_j = 0;
 }
 
 // Lanes without a sample in flight close finished items and take new ones from the wave's
@@ -892,7 +894,24 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
         const unsigned k = (unsigned)__popcll(m), avail = L.pool_end - L.pool_next;
         unsigned fresh = 0;
         if (k > avail) { // wave-uniform: one atomic refills the pool
-            if (lane == 0) fresh = atomicAdd(p.counter, (unsigned)p.pool);
+            if (lane == 0) {
+                if (p.n_split <= 1) {
+                    fresh = atomicAdd(p.counter, (unsigned)p.pool);
+                } else {
+                    // the range of this workgroup's XCD first, then the others in turn (L.split_j: the
+                    // ranges this wave found spent); all spent -> total, which ends the lane
+                    fresh = total;
+                    const unsigned g0 = blockIdx.x & (unsigned)(p.n_split - 1);
+                    for (; L.split_j < (unsigned)p.n_split; L.split_j++) {
+                        const unsigned g = (g0 + L.split_j) & (unsigned)(p.n_split - 1);
+                        const unsigned f = atomicAdd(p.counter + kSplitStride * g, (unsigned)p.pool);
+                        if (f < p.split_start[g + 1] - p.split_start[g]) {
+                            fresh = p.split_start[g] + f;
+                            break;
+                        }
+                    }
+                }
+            }
             fresh = __builtin_amdgcn_readfirstlane(fresh);
         }
         if (need) {

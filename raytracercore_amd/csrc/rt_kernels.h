@@ -5,6 +5,9 @@
 
 namespace rtc {
 
+constexpr int kMaxSplit = 8;     // item ranges of a launch: one per XCD of the MI355X
+constexpr int kSplitStride = 32; // dispenser words apart (one 128-B line each)
+
 // Work decomposition of one path-tracing launch over a w x h tile.
 struct PathParams {
     int x0, y0, w, h;           // tile within the frame
@@ -28,7 +31,11 @@ struct PathParams {
     unsigned long long seed;
     rt_key2 seed_key;           // rt_rng_seed_key(seed) (rtcore_rng.h)
     unsigned long long sample_base;
-    unsigned int* counter;      // work-item dispenser (zeroed before launch), handed out 64 at a time
+    unsigned int* counter;      // work-item dispensers (zeroed before launch), one per item range, kSplitStride apart
+    int n_split;                // item ranges (1 or kMaxSplit): range g = blocks [split_start[g], split_start[g + 1])
+                                // in item units, dealt first to the workgroups b with b % n_split == g (the
+                                // workgroups that share one XCD and its L2), then to any wave once theirs is spent
+    unsigned split_start[9];
     float4* partial;            // [block][chunk][64 pixels]: rgb sums, (samples | misses << 16)
     unsigned long long* rays;   // Scene.RayTrace-equivalents (added to)
     int* stack_ovf;             // BVH kernels: traversal-stack overflow, RT_STACK_OVF entries per lane of the grid

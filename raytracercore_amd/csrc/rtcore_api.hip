@@ -1278,6 +1278,18 @@ PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint6
     if (const char* e = getenv("RTCORE_BVH_REFILL")) p.refill = std::max(1, std::min(64, atoi(e)));
     p.spec = 16;
     if (const char* e = getenv("RTCORE_BVH_SPEC")) p.spec = std::max(1, std::min(64, atoi(e)));
+    // XCD-local item ranges: the 8x8 blocks cut into kMaxSplit runs of consecutive blocks (horizontal
+    // strips of the tile), each dealt first to the workgroups of one XCD, so that one XCD's waves work
+    // on neighbouring pixels and their closest-hit queries share that XCD's L2.  A single range hands
+    // the whole frame out in order to all XCDs at once: every L2 then holds the nodes of the same
+    // band.  RTCORE_XCD_SPLIT=0 turns it off (A/B).
+    p.n_split = 1;
+    const int n_blocks = p.n_pad / 64;
+    int want = kMaxSplit;
+    if (const char* e = getenv("RTCORE_XCD_SPLIT")) want = atoi(e) > 0 ? kMaxSplit : 1;
+    if (want > 1 && n_blocks >= 4 * kMaxSplit) p.n_split = kMaxSplit;
+    for (int g = 0; g <= p.n_split; g++)
+        p.split_start[g] = (unsigned)((int64_t)n_blocks * g / p.n_split) * (unsigned)(p.n_chunks * 64);
     p.seed = seed;
     p.seed_key = rt_rng_seed_key(seed);
     p.sample_base = base;
@@ -1387,7 +1399,7 @@ int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t
         return RT_ERR_ARG;
     }
     HIP_TRY(s->partial.reserve(need));
-    HIP_TRY(s->counter.reserve(1));
+    HIP_TRY(s->counter.reserve(kMaxSplit * kSplitStride));
     p.partial = s->partial.p;
     p.counter = s->counter.p;
     p.rays = d_rays;
@@ -1400,7 +1412,7 @@ int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t
     if (p.ray_log) s->ray_log = nullptr;
     // order after the previous operation when it ran on another stream (shared scratch)
     if (s->any_op && stream != s->last_stream) HIP_TRY(hipStreamWaitEvent(stream, s->done_ev, 0));
-    HIP_TRY(hipMemsetAsync(p.counter, 0, sizeof(unsigned int), stream));
+    HIP_TRY(hipMemsetAsync(p.counter, 0, sizeof(unsigned int) * kSplitStride * p.n_split, stream));
     const int grid = s->n_cu * (s->stats_on ? s->stats_blocks_per_cu : s->blocks_per_cu);
     p.stack_ovf = nullptr;
     if (s->variant >= 4) { // BVH kernels: the stacks' global overflow area
