@@ -172,8 +172,9 @@ typedef enum rt_bvh_builder {
    0 not used, -1 build failed: see rt_scene_get_jit_error), [16] its hiprtc compile ms (0 when
    it came from the cache), [17] 1 if it came from the in-process or on-disk cache,
    [18] primitives per group of the grouped brute-force order (fixed at creation: 8 when the
-   scene-specialised build was on then, else 4) */
-#define RT_BUILD_STATS_COUNT 19
+   scene-specialised build was on then, else 4); [19] leaves of the wide tree, [20] of them compact
+   (primitives of one kind and one set of test flags, read as 48-B records) */
+#define RT_BUILD_STATS_COUNT 21
 
 /* ---------------------------------------------------------------- library ---- */
 int rt_abi_version(void);

@@ -31,7 +31,8 @@ RT_TRAVERSAL_AUTO, RT_TRAVERSAL_BRUTE, RT_TRAVERSAL_BVH, RT_TRAVERSAL_BVH2, RT_T
 RT_BVH_BUILDER_AUTO, RT_BVH_BUILDER_HOST, RT_BVH_BUILDER_GPU = 0, 1, 2
 BUILD_STAT_NAMES = ("prepare_ms", "bvh_ms", "upload_ms", "gpu_build_ms", "ploc_rounds", "wide_nodes", "stack_need",
                     "flat_rects", "flat_boxes", "flat_frames", "flat_frame_boxes", "flat_frame_rects", "flat_tris",
-                    "flat_spheres", "hot_nodes", "jit_status", "jit_compile_ms", "jit_cached", "group_max")
+                    "flat_spheres", "hot_nodes", "jit_status", "jit_compile_ms", "jit_cached", "group_max",
+                    "wide_leaves", "compact_leaves")
 
 
 def set_jit(on: bool) -> None:

@@ -76,14 +76,15 @@ __device__ __forceinline__ int pack_sg(int slot, bool gin) { return (slot << 1) 
 
 // Triangle via the affine inverse record (TestRec): w(t) = 0 gives t, then (u, v).
 // Inside (Moller-Trumbore's 1/det < 0, Triangle.cs:127) <=> d . n > 0 <=> dw > 0.
-__device__ __forceinline__ void hit_tri(const TestRec& R, int slot, V3 o, V3 d, int prev, Best& b)
+// The BVH kernels name the primitive a ray leaves by its slot (SLOT: id = slot, Sample.prev = slot),
+// so that the records of compact leaves carry no ID; the brute-force kernels by its primitive ID.
+__device__ __forceinline__ void hit_tri_rows(float4 r0, float4 r1, float4 r2, uint32_t fl, int id, int slot, V3 o, V3 d,
+                                             int prev, Best& b)
 {
-    const int id = __float_as_int(R.meta.x);
-    const uint32_t fl = __float_as_uint(R.meta.y);
-    const float dw = dot3(R.r2, d);
-    const float t = -dot4(R.r2, o) * rcp(dw);
-    const float u = fmaf(t, dot3(R.r0, d), dot4(R.r0, o));
-    const float v = fmaf(t, dot3(R.r1, d), dot4(R.r1, o));
+    const float dw = dot3(r2, d);
+    const float t = -dot4(r2, o) * rcp(dw);
+    const float u = fmaf(t, dot3(r0, d), dot4(r0, o));
+    const float v = fmaf(t, dot3(r1, d), dot4(r1, o));
     const bool gin = dw > 0.0f;
     bool ok = (t >= 0.0f) & (t < b.t) & (u >= 0.0f) & (v >= 0.0f) & (id != prev);
     ok &= (fl & F_MIRROR) ? ((u <= 1.0f) & (v <= 1.0f)) : (u + v <= 1.0f);
@@ -91,27 +92,31 @@ __device__ __forceinline__ void hit_tri(const TestRec& R, int slot, V3 o, V3 d, 
     b.t = ok ? t : b.t;
     b.sg = ok ? pack_sg(slot, gin) : b.sg;
 }
+template <bool SLOT = false>
+__device__ __forceinline__ void hit_tri(const TestRec& R, int slot, V3 o, V3 d, int prev, Best& b)
+{
+    hit_tri_rows(R.r0, R.r1, R.r2, __float_as_uint(R.meta.y), SLOT ? slot : __float_as_int(R.meta.x), slot, o, d, prev, b);
+}
 
 // Sphere (Sphere.cs:50-155).  Primitive.RayTrace returns the first surviving root: the close
 // one (Inside = false) if it lies ahead and is not culled, otherwise the far one.
 template <class XfP> // const XformF*, generic or in the constant address space
-__device__ __forceinline__ void hit_sph(const TestRec& R, int slot, V3 o, V3 d, int prev, XfP xf, Best& b)
+__device__ __forceinline__ void hit_sph_rows(float4 r0, float4 r1, uint32_t fl, int id, int slot, V3 o, V3 d, int prev,
+                                             XfP xf, Best& b)
 {
-    const int id = __float_as_int(R.meta.x);
-    const uint32_t fl = __float_as_uint(R.meta.y);
     V3 oo = o, dd = d;
     float k = 1.0f; // object-space ray parameter -> world distance
     if (fl & F_TRANSFORMED) {
-        const XformF X = xf[__float_as_int(R.r1.y)];
+        const XformF X = xf[__float_as_int(r1.y)];
         oo = xf_point(X.to_world, o);
         const V3 dl = xf_dir(X.to_world, d);
         k = __builtin_amdgcn_rsqf(dot(dl, dl)); // |to_obj * dd| = 1 / |to_world * d|
         dd = dl * k;
     }
-    const V3 oc = oo - xyz(R.r0);
+    const V3 oc = oo - xyz(r0);
     const float bb = dot(oc, dd);
     const V3 l = madd(dd, -bb, oc);
-    const float disc = R.r1.x - dot(l, l);
+    const float disc = r1.x - dot(l, l);
     const bool self = id == prev;
     const float sq = fsqrt(fmaxf(disc, 0.0f));
     // self-hit: the root at the bounce point is skipped; the other root is -2 (oc.dd)
@@ -127,11 +132,17 @@ __device__ __forceinline__ void hit_sph(const TestRec& R, int slot, V3 o, V3 d, 
     b.t = ok ? tw : b.t;
     b.sg = ok ? pack_sg(slot, use_far) : b.sg;
 }
+template <bool SLOT = false, class XfP>
+__device__ __forceinline__ void hit_sph(const TestRec& R, int slot, V3 o, V3 d, int prev, XfP xf, Best& b)
+{
+    hit_sph_rows(R.r0, R.r1, __float_as_uint(R.meta.y), SLOT ? slot : __float_as_int(R.meta.x), slot, o, d, prev, xf, b);
+}
 
 // Plane (Plane.cs:36-66), including the NearlyEqual branch for rays in the plane.
+template <bool SLOT = false>
 __device__ __forceinline__ void hit_plane(const TestRec& R, int slot, V3 o, V3 d, int prev, Best& b)
 {
-    const int id = __float_as_int(R.meta.x);
+    const int id = SLOT ? slot : __float_as_int(R.meta.x);
     const uint32_t fl = __float_as_uint(R.meta.y);
     const V3 n = xyz(R.r0);
     const float pd = R.r0.w;
@@ -342,15 +353,36 @@ __device__ __forceinline__ void trace_brute(const SceneT& s, GroupP groups, Test
     }
 }
 
-template <class XfP>
+template <bool SLOT = false, class XfP>
 __device__ __forceinline__ void hit_any(const TestRec& R, int slot, V3 o, V3 d, int prev, XfP xf, Best& b)
 {
     switch (__float_as_uint(R.meta.y) & KIND_MASK) {
-    case RT_PRIM_TRIANGLE: hit_tri(R, slot, o, d, prev, b); break;
-    case RT_PRIM_SPHERE: hit_sph(R, slot, o, d, prev, xf, b); break;
-    default: hit_plane(R, slot, o, d, prev, b); break;
+    case RT_PRIM_TRIANGLE: hit_tri<SLOT>(R, slot, o, d, prev, b); break;
+    case RT_PRIM_SPHERE: hit_sph<SLOT>(R, slot, o, d, prev, xf, b); break;
+    default: hit_plane<SLOT>(R, slot, o, d, prev, b); break;
     }
 }
+
+// The pending leaf of a BVH query is one register: the leaf code (rt_internal.h) whose count field
+// holds the primitives still to test, minus one; -1 when no leaf is pending.  A leaf step decodes
+// its slots and, for a compact leaf, the record flags its primitives share (leaf_flags);
+// kLeafGeneric for a generic leaf (flags from each record's meta row).
+constexpr uint32_t kLeafGeneric = 0xFFFFFFFFu;
+__device__ __forceinline__ void leaf_decode(int pend, int& k, int& kend, uint32_t& lfl)
+{
+    const bool compact = (pend & kLeafCompact) != 0;
+    k = compact ? (pend >> 2) & (kLeafCompactMaxFirst - 1) : pend >> 3;
+    kend = k + (pend & (compact ? 3 : 7)) + 1;
+    lfl = compact ? leaf_flags(((uint32_t)pend >> 25) & 31u) : kLeafGeneric;
+}
+// after a step of n primitives: the first slot advanced by n and the count field lowered by n, or -1
+__device__ __forceinline__ int leaf_advance(int pend, int n)
+{
+    const bool compact = (pend & kLeafCompact) != 0;
+    const int left = pend & (compact ? 3 : 7);
+    return left >= n ? pend + (compact ? (n << 2) - n : (n << 3) - n) : -1;
+}
+
 
 
 // One visit of a 4-wide quantised node (Node4Q): slab tests of the four children against
@@ -375,7 +407,7 @@ __device__ __forceinline__ void cswap(float& da, int& ra, float& db, int& rb)
 // load, plus the pointer arithmetic, on every push and pop, and through the texture addresser).
 // The bases are wave-uniform and the lane's offset is formed at use: per-lane pointers held across
 // the loop were spilled to scratch and reloaded at every push (C4 52.4 -> 66.6 ms).
-#define RT_STACK_OVF 40
+#define RT_STACK_OVF 44 // = kStackOverflow (rt_kernels.h); with the 16-entry LDS stacks, 60 entries in all
 typedef __attribute__((address_space(3))) int LdsInt;
 typedef __attribute__((address_space(1))) int GlobalInt;
 struct TravStack {
@@ -642,7 +674,7 @@ __device__ __forceinline__ Best query_start(const SceneT& s, int prev)
 
 // One bounce of Raytracer.GetColor after the closest-hit query.  Returns 0 to continue the
 // path, 1 if the sample ended with colour `col`, 2 if it ended as a miss (Placeholder).
-template <bool VN, bool PIN = false, class SceneT, class VnP, class TestP>
+template <bool VN, bool PIN = false, bool SLOT = false, class SceneT, class VnP, class TestP>
 __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ prims, const MatF* __restrict__ mats,
                                      const XformF* __restrict__ xfs, VnP vnormals, TestP tests, const PrimD* prims_d,
                                      const Best& b, Sample& S, V3& col)
@@ -767,7 +799,7 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
     }
     S.o = pos;
     S.d = normalize(out_dir);
-    S.prev = id;
+    S.prev = SLOT ? (b.sg >> 1) : id; // the BVH kernels name the left primitive by its slot
     if (VN && s.n_vn > 0 && kind == RT_PRIM_TRIANGLE && (fl & F_HASNORMALS)) {
         // does the reference's next query meet this triangle again (vn_rehit_test), and is that a
         // new hit?  Primitive.RayTrace culls it first when one-sided (Primitive.cs:56-64).  A NaN
@@ -793,21 +825,23 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
 #define RT_GROUPED_WAVES 7 // the same for the grouped brute-force kernel
 #endif
 #ifndef RT_WIDE_STACK
-#define RT_WIDE_STACK 20 // LDS entries of the wide BVH kernel's traversal stack (then global overflow)
+#define RT_WIDE_STACK 16 // LDS entries of the wide BVH kernel's traversal stack (then global overflow): 7 blocks per CU
 #endif
 #ifndef RT_BVH_SPEC
 #define RT_BVH_SPEC 1 // speculative BVH traversal with wave-wide leaf steps (p.spec); 0: the mixed-step loop (C4 69.8 -> 62.1 ms)
 #endif
 #ifndef RT_SPEC_PRIMS
-#define RT_SPEC_PRIMS 2 // leaf primitives per leaf step of the speculative traversal (<= kTestSpares + 1)
-#endif
-#ifndef RT_LEAF_STEP
-#define RT_LEAF_STEP 2 // leaf primitives tested per BVH traversal step
+#define RT_SPEC_PRIMS 2 // leaf primitives per leaf step, both traversal loops (<= kTestSpares + 1)
 #endif
 #ifndef RT_BVH_WAVES
-#define RT_BVH_WAVES 6 // the same for the BVH kernels (C4: 4 waves with a 40-entry LDS stack 80.7 ms, 5 waves with 24 entries
+#define RT_BVH_WAVES 7 // the same for the BVH kernels (C4: 4 waves with a 40-entry LDS stack 80.7 ms, 5 waves with 24 entries
                        // 72.0 ms; with the launch record read at use, 6 waves with 20 entries (8 VGPRs spilled) 57.2-58.6
-                       // against 60.7-61.3 ms at 5 / 24; 7 waves with 16 entries spill 27 VGPRs: 70.1 ms)
+                       // against 60.7-61.3 ms at 5 / 24; 7 waves with 16 entries spilled 27 VGPRs: 70.1 ms.  Round 3,
+                       // after compact leaves (one register of pending-leaf state) and o/d recomputed per node visit:
+                       // 6 waves / 20 entries 45.9 ms (2 spilled), 7 waves / 16 entries 45.0 ms (17 spilled))
+#endif
+#ifndef RT_BVH2_WAVES
+#define RT_BVH2_WAVES 6 // the BVH2 kernel (24-entry LDS stack: at most 6 blocks per CU)
 #endif
 
 // LDS staging of the shading records (PrimF per slot, MatF per ID, XformF): the per-lane gathers
@@ -987,12 +1021,12 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
 }
 
 // After a closest-hit query: one bounce of GetColor; a finished sample goes into the item's sums.
-template <bool VN, bool PIN = false, class SceneT, class VnP, class TestP>
+template <bool VN, bool PIN = false, bool SLOT = false, class SceneT, class VnP, class TestP>
 __device__ __forceinline__ void bounce(Lane& L, Sample& S, const SceneT& s, const ShadeRecs& R, VnP vnormals, TestP tests,
                                        const PrimD* prims_d, const Best& b)
 {
     V3 col;
-    const int r = shade<VN, PIN>(s, R.prims, R.mats, R.xfs, vnormals, tests, prims_d, b, S, col);
+    const int r = shade<VN, PIN, SLOT>(s, R.prims, R.mats, R.xfs, vnormals, tests, prims_d, b, S, col);
     if (r != 0) {
         const bool hit = r == 1;
         L.ar += hit ? col.x : 0.0f;
@@ -1176,6 +1210,55 @@ __global__ void __launch_bounds__(256, CULL ? RT_GROUPED_WAVES : RT_PATH_WAVES)
     path_body<CULL, LDS, STATS, VN>(camp, pp); // the other arguments are the BVH kernels' (same launch)
 }
 
+// One leaf step of the BVH kernels: RT_SPEC_PRIMS primitives of the pending leaf pend, their
+// loads issued together.  Every leaf reads the 48-B rows of its records (3 loads per primitive); a
+// compact leaf's flags come with its reference (lfl), a generic leaf's from each record's meta row
+// (one more 4-B load).  The BVH order holds triangles and spheres only (planes follow it), and both
+// arrays carry kTestSpares zero records after the last slot.
+template <bool STATS, class TestP, class RowP, class XfP>
+__device__ __forceinline__ void test_leaf(TestP tests, RowP rows, XfP xf, int pend, V3 o, V3 d, int prev, Best& b,
+                                          unsigned& n_tri, unsigned& n_sph)
+{
+    int k, kend;
+    uint32_t lfl;
+    leaf_decode(pend, k, kend, lfl);
+    float4 r[RT_SPEC_PRIMS][3];
+    uint32_t fl[RT_SPEC_PRIMS];
+#pragma unroll
+    for (int j = 0; j < RT_SPEC_PRIMS; j++) {
+        r[j][0] = rows[3 * (k + j)];
+        r[j][1] = rows[3 * (k + j) + 1];
+        r[j][2] = rows[3 * (k + j) + 2];
+    }
+    if (lfl == kLeafGeneric) {
+#pragma unroll
+        for (int j = 0; j < RT_SPEC_PRIMS; j++) fl[j] = __float_as_uint(tests[k + j].meta.y);
+    } else {
+#pragma unroll
+        for (int j = 0; j < RT_SPEC_PRIMS; j++) fl[j] = lfl;
+    }
+    // all rows in registers before the kind dispatch: otherwise the compiler sinks row loads into the
+    // triangle / sphere branches, one more round trip per step (C4 49.9 -> 48.9 ms, 64-B records)
+#pragma unroll
+    for (int j = 0; j < RT_SPEC_PRIMS; j++) {
+        pin4(r[j][0]);
+        pin4(r[j][1]);
+        pin4(r[j][2]);
+    }
+#pragma unroll
+    for (int j = 0; j < RT_SPEC_PRIMS; j++) {
+        if (j == 0 || k + j < kend) {
+            const bool sph = (fl[j] & KIND_MASK) == RT_PRIM_SPHERE;
+            if (STATS) {
+                if (sph) n_sph++;
+                else n_tri++;
+            }
+            if (sph) hit_sph_rows(r[j][0], r[j][1], fl[j], k + j, k + j, o, d, prev, xf, b);
+            else hit_tri_rows(r[j][0], r[j][1], r[j][2], fl[j], k + j, k + j, o, d, prev, b);
+        }
+    }
+}
+
 // BVH megakernel with decoupled traversal.  A loop iteration advances the traversing lanes by
 // one step: with RT_BVH_SPEC a wave-wide node step or leaf step (up to two primitives), lanes
 // keeping a reached leaf pending while they visit further nodes; without it, one node visit or
@@ -1184,7 +1267,7 @@ __global__ void __launch_bounds__(256, CULL ? RT_GROUPED_WAVES : RT_PATH_WAVES)
 // traversal no longer holds the other 63 lanes of its wave, and the divergent shading code is
 // paid once per batch of finished queries.
 template <int WIDTH, int STACK, bool LDS, bool STATS, bool VN>
-__global__ void __launch_bounds__(256, RT_BVH_WAVES)
+__global__ void __launch_bounds__(256, WIDTH == 4 ? RT_BVH_WAVES : RT_BVH2_WAVES)
     path_kernel_bvh(PathScene, const CameraF* __restrict__ camp, const PathParams* __restrict__ pp, const TestRec*,
                     const RectRec*, const FrameRec*, const PrimF*, const NodeF*, const Node4Q*, const GroupRec*,
                     const XformF*, const MatF*, const float4*)
@@ -1217,8 +1300,12 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
     // traversal state of the lane's current query
     bool trav = false, done = false;
     [[maybe_unused]] bool more = false; // RT_BVH_SPEC: ref still holds a reference to process (stack not exhausted)
-    int ref = 0, sp = 0, k = 0, kend = 0; // [k, kend): primitives of the leaf being tested
-    V3 id{0, 0, 0}, oi{0, 0, 0}; // 1/d and o/d of the query
+    int ref = 0, sp = 0;
+    int pend = -1; // the pending leaf (leaf_decode), -1 for none
+    // 1/d of the query; o/d is recomputed per node visit (three multiplies) instead of being held
+    // across the loop (VGPR spills of the C4 kernel 13 -> 2 at 6 waves per SIMD; recomputing 1/d as
+    // well, three clamped reciprocals per visit, measured slower: 45.9 -> 46.2 ms)
+    V3 id{0, 0, 0};
     Best b{__builtin_huge_valf(), -1};
 
     while (true) {
@@ -1229,6 +1316,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
         const ParamsC& p = *pq;
         const auto& s = pq->scene;
         const auto tests = (const RT_AS_CONST TestRec*)pq->tests;
+        const auto rows = (const RT_AS_CONST float4*)pq->rows;
         const auto xf = (const RT_AS_CONST XformF*)pq->xf;
         const auto vnormals = (const RT_AS_CONST float4*)pq->vnormals;
         const auto nodes = (const RT_AS_CONST NodeF*)pq->nodes;
@@ -1241,7 +1329,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
             if (done) { // the query finished: planes (outside the BVH), then one bounce
                 for (int i = s.n_bvh; i < s.n_bvh + s.n_pln; i++) {
                     const TestRec tr = tests[i];
-                    hit_plane(tr, i, S.o, S.d, S.prev, b);
+                    hit_plane<true>(tr, i, S.o, S.d, S.prev, b);
                 }
                 if (STATS && p.ray_log) { // rt_debug_ray_log: the query and its closest hit
                     const unsigned q = atomicAdd(p.ray_log_n, 1u);
@@ -1252,20 +1340,18 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                         r[2] = make_float4(b.t, __int_as_float(b.sg), __int_as_float(S.bounce), 0.0f);
                     }
                 }
-                bounce<VN, !LDS>(L, S, s, R, vnormals, tests, pq->prims_d, b);
+                bounce<VN, !LDS, true>(L, S, s, R, vnormals, tests, pq->prims_d, b);
                 done = false;
             }
             refill<true>(L, S, p, s, *cp, lane, total);
             if (L.live && !trav) { // start the next query
                 id = v3(slab_rcp(S.d.x), slab_rcp(S.d.y), slab_rcp(S.d.z));
-                oi = S.o * id;
                 ref = s.root;
                 sp = 0;
-                k = kend = 0;
+                pend = -1;
                 more = true;
                 if (ref < 0) { // the root itself is a leaf
-                    k = (~ref) >> 3;
-                    kend = k + ((~ref) & 7) + 1;
+                    pend = ~ref;
                     more = false;
                 }
                 b = query_start<VN>(s, S.prev);
@@ -1279,43 +1365,26 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
         // node, so an iteration is one kind of step instead of both.  Node culling uses the best hit
         // so far (the pending leaf not yet tested): more visits, the same closest hit.
         const bool can_node = trav && more && ref >= 0;
-        const bool blocked = trav && k < kend && !can_node;
+        const bool blocked = trav && pend >= 0 && !can_node;
         const bool leaf_step = __ballot(can_node) == 0 || __popcll(__ballot(blocked)) >= p.spec; // wave-uniform
         if (STATS) { // lane slots of this iteration (the BVH kernels reuse the brute-force cycle counters):
                      // testing a leaf | traversing but idle in this step's kind | waiting for the shading phase
             const unsigned n_trav = (unsigned)__popcll(__ballot(trav));
             const unsigned n_node = leaf_step ? 0u : (unsigned)__popcll(__ballot(can_node));
-            const unsigned n_leaf = leaf_step ? (unsigned)__popcll(__ballot(trav && k < kend)) : 0u;
+            const unsigned n_leaf = leaf_step ? (unsigned)__popcll(__ballot(trav && pend >= 0)) : 0u;
             cnt.cyc_start += n_leaf;
             cnt.cyc_trace += n_trav - n_node - n_leaf;
             cnt.cyc_shade += (unsigned)__popcll(__ballot(!trav && (L.active || L.live)));
         }
         if (trav) {
             if (leaf_step) {
-                if (k < kend) { // RT_SPEC_PRIMS primitives of the pending leaf, their loads issued together
-                    TestRec r[RT_SPEC_PRIMS];
-#pragma unroll
-                    for (int j = 0; j < RT_SPEC_PRIMS; j++) r[j] = tests[k + j]; // kTestSpares zero records follow the last leaf
-                    // all rows in registers before the kind dispatch: otherwise the compiler sinks
-                    // row loads into the triangle / sphere branches, one more round trip per step
-                    // (C4 49.9 -> 48.9 ms; fetching the second record only when the leaf has one, by
-                    // an out-of-range buffer offset, measured no further change)
-#pragma unroll
-                    for (int j = 0; j < RT_SPEC_PRIMS; j++) pin_rec(r[j]);
-#pragma unroll
-                    for (int j = 0; j < RT_SPEC_PRIMS; j++) {
-                        if (j == 0 || k + j < kend) {
-                            if (STATS) {
-                                if ((__float_as_uint(r[j].meta.y) & KIND_MASK) == RT_PRIM_TRIANGLE) cnt.tris++;
-                                else cnt.sphs++;
-                            }
-                            hit_any(r[j], k + j, S.o, S.d, S.prev, xf, b);
-                        }
-                    }
-                    k += RT_SPEC_PRIMS;
+                if (pend >= 0) { // RT_SPEC_PRIMS primitives of the pending leaf, their loads issued together
+                    test_leaf<STATS>(tests, rows, xf, pend, S.o, S.d, S.prev, b, cnt.tris, cnt.sphs);
+                    pend = leaf_advance(pend, RT_SPEC_PRIMS);
                 }
             } else if (can_node) {
                 bool pop = true;
+                const V3 oi = S.o * id;
                 if (WIDTH == 4) {
                     const Node4Q q = (ref & RT_HOT_BIT) ? lds_hot[ref & ~RT_HOT_BIT] : Node4Q(nodes4[ref]);
                     wide_visit<STACK>(q, id, oi, b.t, ref, sp, stk, pop);
@@ -1343,14 +1412,12 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
             }
             // a leaf reference becomes the pending leaf once the previous one is tested, and the
             // next reference is popped so that traversal goes on past it
-            if (more && ref < 0 && k >= kend) {
-                const int code = ~ref;
-                k = code >> 3;
-                kend = k + (code & 7) + 1;
+            if (more && ref < 0 && pend < 0) {
+                pend = ~ref;
                 if (sp > 0) ref = pop_ref<STACK>(stk, sp);
                 else more = false;
             }
-            if (!more && k >= kend) {
+            if (!more && pend < 0) {
                 trav = false;
                 done = true;
             }
@@ -1358,36 +1425,20 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
 #else
         if (trav) { // one traversal step: one node visit, or one primitive of the current leaf
             bool pop = true; // child references are node indices or ~leaf codes (any int)
-            if (k < kend) { // up to RT_LEAF_STEP primitives, their loads issued together
-                const TestRec r0 = tests[k];
-#if RT_LEAF_STEP >= 2
-                const TestRec r1 = tests[k + 1]; // the record array carries a spare at the end
-#endif
-                if (STATS) {
-                    if ((__float_as_uint(r0.meta.y) & KIND_MASK) == RT_PRIM_TRIANGLE) cnt.tris++;
-                    else cnt.sphs++;
-                }
-                hit_any(r0, k, S.o, S.d, S.prev, xf, b);
-#if RT_LEAF_STEP >= 2
-                if (k + 1 < kend) {
-                    if (STATS) {
-                        if ((__float_as_uint(r1.meta.y) & KIND_MASK) == RT_PRIM_TRIANGLE) cnt.tris++;
-                        else cnt.sphs++;
-                    }
-                    hit_any(r1, k + 1, S.o, S.d, S.prev, xf, b);
-                }
-#endif
-                k += RT_LEAF_STEP;
-                pop = k >= kend;
+            if (pend >= 0) { // RT_SPEC_PRIMS primitives, their loads issued together
+                test_leaf<STATS>(tests, rows, xf, pend, S.o, S.d, S.prev, b, cnt.tris, cnt.sphs);
+                pend = leaf_advance(pend, RT_SPEC_PRIMS);
+                pop = pend < 0;
             } else if (WIDTH == 4) {
                 // the top of the tree comes from LDS, the rest from global memory
                 const Node4Q q = (ref & RT_HOT_BIT) ? lds_hot[ref & ~RT_HOT_BIT] : Node4Q(nodes4[ref]);
-                wide_visit<STACK>(q, id, oi, b.t, ref, sp, stk, pop);
+                wide_visit<STACK>(q, id, S.o * id, b.t, ref, sp, stk, pop);
                 if (STATS) cnt.nodes++;
             } else {
                 const NodeF n = nodes[ref];
                 if (STATS) cnt.nodes++;
                 float tl, tr;
+                const V3 oi = S.o * id;
                 const bool hl = slab(n.lmin, n.lmax, oi, id, b.t, tl);
                 const bool hr = slab(n.rmin, n.rmax, oi, id, b.t, tr);
                 const int cl = __float_as_int(n.lmin.w), cr = __float_as_int(n.rmin.w);
@@ -1409,11 +1460,7 @@ __global__ void __launch_bounds__(256, RT_BVH_WAVES)
                     done = true;
                 }
             }
-            if (trav && ref < 0 && k >= kend) { // entering a leaf: its primitives come one per step
-                const int code = ~ref;
-                k = code >> 3;
-                kend = k + (code & 7) + 1;
-            }
+            if (trav && ref < 0 && pend < 0) pend = ~ref; // entering a leaf
         }
 #endif
         if (STATS) {
@@ -1440,10 +1487,12 @@ __global__ void __launch_bounds__(256, WAVES) trace_rays_kernel(TraceRaysParams 
     const TravStack stk = make_stack(stack_mem, p.stack_ovf);
     const int lane = threadIdx.x & 63;
     const RT_AS_CONST TestRec* tests = (const RT_AS_CONST TestRec*)p.tests;
+    const RT_AS_CONST float4* rows = (const RT_AS_CONST float4*)p.rows;
     const RT_AS_CONST Node4Q* nodes4 = (const RT_AS_CONST Node4Q*)p.nodes4;
     const RT_AS_CONST XformF* xf = (const RT_AS_CONST XformF*)p.xf;
     bool trav = false, more = false, exhausted = false;
-    int ref = 0, sp = 0, k = 0, kend = 0, prev = -1;
+    int ref = 0, sp = 0, pend = -1, prev = -1;
+    unsigned n_tri = 0, n_sph = 0;
     unsigned idx = 0, pool_next = 0, pool_end = 0; // the wave's pool of ray indices (uniform)
     V3 o{0, 0, 0}, d{0, 0, 0}, id{0, 0, 0}, oi{0, 0, 0};
     Best b{__builtin_huge_valf(), -1};
@@ -1472,11 +1521,10 @@ __global__ void __launch_bounds__(256, WAVES) trace_rays_kernel(TraceRaysParams 
                     oi = o * id;
                     ref = p.root4;
                     sp = 0;
-                    k = kend = 0;
+                    pend = -1;
                     more = true;
                     if (ref < 0) {
-                        k = (~ref) >> 3;
-                        kend = k + ((~ref) & 7) + 1;
+                        pend = ~ref;
                         more = false;
                     }
                     b = Best{__builtin_huge_valf(), -1};
@@ -1492,25 +1540,18 @@ __global__ void __launch_bounds__(256, WAVES) trace_rays_kernel(TraceRaysParams 
         }
         if (!__any(trav)) break;
         const bool can_node = trav && more && ref >= 0;
-        const bool blocked = trav && k < kend && !can_node;
+        const bool blocked = trav && pend >= 0 && !can_node;
         const bool leaf_step = __ballot(can_node) == 0 || __popcll(__ballot(blocked)) >= p.spec;
         if (STATS) {
             n_slots += 64;
-            if (leaf_step) n_leaf += (trav && k < kend) ? 1 : 0;
+            if (leaf_step) n_leaf += (trav && pend >= 0) ? 1 : 0;
             else n_node += can_node ? 1 : 0;
         }
         if (trav) {
             if (leaf_step) {
-                if (k < kend) {
-                    TestRec r[RT_SPEC_PRIMS];
-#pragma unroll
-                    for (int j = 0; j < RT_SPEC_PRIMS; j++) r[j] = tests[k + j];
-#pragma unroll
-                    for (int j = 0; j < RT_SPEC_PRIMS; j++) pin_rec(r[j]);
-#pragma unroll
-                    for (int j = 0; j < RT_SPEC_PRIMS; j++)
-                        if (j == 0 || k + j < kend) hit_any(r[j], k + j, o, d, prev, xf, b);
-                    k += RT_SPEC_PRIMS;
+                if (pend >= 0) {
+                    test_leaf<false>(tests, rows, xf, pend, o, d, prev, b, n_tri, n_sph);
+                    pend = leaf_advance(pend, RT_SPEC_PRIMS);
                 }
             } else if (can_node) {
                 bool pop = true;
@@ -1521,14 +1562,12 @@ __global__ void __launch_bounds__(256, WAVES) trace_rays_kernel(TraceRaysParams 
                     else more = false;
                 }
             }
-            if (more && ref < 0 && k >= kend) {
-                const int code = ~ref;
-                k = code >> 3;
-                kend = k + (code & 7) + 1;
+            if (more && ref < 0 && pend < 0) {
+                pend = ~ref;
                 if (sp > 0) ref = pop_ref<STACK>(stk, sp);
                 else more = false;
             }
-            if (!more && k >= kend) {
+            if (!more && pend < 0) {
                 trav = false;
                 p.hits[idx] = make_float2(b.t, __int_as_float(b.sg));
             }
@@ -1642,6 +1681,55 @@ __global__ void tile_host_layout_kernel(int w, int h, const double* __restrict__
     rgb[3 * o + 2] = sum[2 * npix + i];
     on[o] = ns[i];
     om[o] = ms[i];
+}
+
+// ---- compact leaves (rt_internal.h): 48-B rows and homogeneous leaf references --------------
+__global__ void rows_kernel(const TestRec* __restrict__ tests, int n, float4* __restrict__ rows)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const TestRec t = tests[i];
+    rows[3 * (size_t)i] = t.r0;
+    rows[3 * (size_t)i + 1] = t.r1;
+    rows[3 * (size_t)i + 2] = t.r2;
+}
+
+// A generic leaf whose primitives (at most 4, from slot < 2^23) share their kind (triangle or sphere)
+// and test flags becomes a compact leaf; any other reference is returned unchanged.
+__device__ int compact_ref(int ref, const TestRec* __restrict__ tests)
+{
+    if (ref >= 0 || ref == RT_NODE4_EMPTY) return ref;
+    const int code = ~ref;
+    if (code & kLeafCompact) return ref;
+    const int first = code >> 3, count = (code & 7) + 1;
+    if (count > 4 || first >= kLeafCompactMaxFirst) return ref;
+    uint32_t key = 0;
+    for (int j = 0; j < count; j++) {
+        const uint32_t fl = __float_as_uint(tests[first + j].meta.y), kind = fl & KIND_MASK;
+        if (kind != RT_PRIM_TRIANGLE && kind != RT_PRIM_SPHERE) return ref;
+        const uint32_t lf = (kind == RT_PRIM_SPHERE ? 1u : 0u) | ((fl >> 1) & 0xEu) | ((fl >> 2) & 0x10u);
+        if (j > 0 && lf != key) return ref;
+        key = lf;
+    }
+    return ~(kLeafCompact | (int)(key << 25) | (first << 2) | (count - 1));
+}
+
+__global__ void compact_nodes_kernel(NodeF* __restrict__ n2, int n_n2, Node4Q* __restrict__ n4, int n_n4,
+                                     const TestRec* __restrict__ tests)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_n2) {
+        NodeF& n = n2[i];
+        n.lmin.w = __int_as_float(compact_ref(__float_as_int(n.lmin.w), tests));
+        n.rmin.w = __int_as_float(compact_ref(__float_as_int(n.rmin.w), tests));
+    }
+    if (i < n_n4) {
+        Node4Q& q = n4[i];
+        q.c.z = __int_as_float(compact_ref(__float_as_int(q.c.z), tests));
+        q.c.w = __int_as_float(compact_ref(__float_as_int(q.c.w), tests));
+        q.d.x = __int_as_float(compact_ref(__float_as_int(q.d.x), tests));
+        q.d.y = __int_as_float(compact_ref(__float_as_int(q.d.y), tests));
+    }
 }
 
 using PathKernel = void (*)(PathScene, const CameraF*, const PathParams*, const TestRec*, const RectRec*, const FrameRec*, const PrimF*,
@@ -1774,6 +1862,7 @@ void fill_launch(const DevScene& s, int variant, PathParams& p)
     ps.n_slots = ps.n_bvh + s.n_pln;
     p.scene = ps;
     p.tests = bvh ? s.tests_bvh : grouped ? s.tests_gr : s.tests_bf;
+    p.rows = bvh ? s.rows_bvh : nullptr;
     p.rects = grouped ? s.rects_gr : s.rects_bf;
     p.frames = grouped ? s.frames_gr : s.frames_bf;
     p.prims = bvh ? s.prims_bvh : grouped ? s.prims_gr : s.prims_bf;
@@ -1860,6 +1949,18 @@ int trace_rays_blocks_per_cu(int waves)
 hipError_t launch_trace_rays(const TraceRaysParams& p, int waves, int grid_blocks, hipStream_t stream)
 {
     hipLaunchKernelGGL(pick_trace(waves, p.stats != nullptr), dim3(grid_blocks), dim3(256), 0, stream, p);
+    return hipGetLastError();
+}
+
+hipError_t compact_leaves(const TestRec* d_tests, int n_records, float4* d_rows, NodeF* d_nodes, int n_nodes,
+                          Node4Q* d_nodes4, int n_nodes4, bool rewrite, hipStream_t stream)
+{
+    if (n_records > 0)
+        hipLaunchKernelGGL(rows_kernel, dim3((n_records + 255) / 256), dim3(256), 0, stream, d_tests, n_records, d_rows);
+    const int n = std::max(n_nodes, n_nodes4);
+    if (rewrite && n > 0)
+        hipLaunchKernelGGL(compact_nodes_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_nodes, n_nodes, d_nodes4,
+                           n_nodes4, d_tests);
     return hipGetLastError();
 }
 

@@ -190,7 +190,27 @@ struct PathScene {
     float ambient_r, ambient_g, ambient_b;
 };
 
-// Child reference in a NodeF: >= 0 internal node index, < 0 leaf = ~(first << 3 | (count-1)).
+// Child reference in a NodeF: >= 0 internal node index, < 0 leaf = ~code, where code is
+//   generic leaf: first << 3 | (count - 1)            (first < 2^27; 64-B TestRecs, kind and flags per record)
+//   compact leaf: kLeafCompact | lf << 25 | first << 2 | (count - 1)   (count <= 4, first < 2^23)
+// A compact leaf's primitives share their kind and test flags, held in the reference (lf: bit 0 sphere,
+// bit 1 Mirror, 2 TwoSided, 3 Invert, 4 transformed), so the leaf step reads only their 48-B rows
+// (the TestRec without its meta row: 3 vector loads per primitive instead of 4).  The builders emit
+// generic leaves; compact_leaves (kernels_path.hip) rewrites every homogeneous one after the upload.
+constexpr int kLeafCompact = 1 << 30;
+constexpr int kLeafCompactMaxFirst = 1 << 23;
+__host__ __device__ inline void leaf_range(int ref, int& first, int& count)
+{
+    const int code = ~ref;
+    const bool compact = (code & kLeafCompact) != 0;
+    first = compact ? (code >> 2) & (kLeafCompactMaxFirst - 1) : code >> 3;
+    count = (code & (compact ? 3 : 7)) + 1;
+}
+// the record flags (KIND_MASK | F_MIRROR | F_TWOSIDED | F_INVERT | F_TRANSFORMED) of a compact leaf
+__host__ __device__ inline uint32_t leaf_flags(uint32_t lf)
+{
+    return ((lf & 1u) ? 1u : 0u) /* RT_PRIM_SPHERE */ | ((lf & 0xEu) << 1) | ((lf & 0x10u) << 2);
+}
 struct alignas(16) NodeF {      // 64 B: both children's boxes
     float4 lmin; // xyz, w = bitcast int left child
     float4 lmax; // xyz, w unused
@@ -304,6 +324,7 @@ struct DevScene {
     int32_t n_tri, n_sph, n_pln; // flat-order slots: n_tri counts general triangles (frame rects included)
     int32_t pln0_bf, pln0_gr, pln0_bvh; // first plane slot of the flat, grouped and BVH orders
     const TestRec* tests_bvh;
+    const float4* rows_bvh;     // the BVH order's TestRecs without the meta row (3 float4 per slot): compact leaves
     const PrimF* prims_bvh;
     const NodeF* nodes;
     int32_t n_nodes;

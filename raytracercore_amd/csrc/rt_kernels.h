@@ -46,6 +46,7 @@ struct PathParams {
     // SGPRs as kernel arguments for the whole kernel (which spilled into VGPR lanes).
     PathScene scene;
     const TestRec* tests;
+    const float4* rows;         // BVH kernels: 3 float4 per slot, the compact leaves' records (DevScene::rows_bvh)
     const RectRec* rects;
     const FrameRec* frames;
     const PrimF* prims;
@@ -70,6 +71,7 @@ struct TraceRaysParams {
     unsigned int* counter;      // ray dispenser (zeroed before the launch)
     int* stack_ovf;
     const TestRec* tests;
+    const float4* rows;
     const Node4Q* nodes4;
     const XformF* xf;
     int root4;
@@ -86,10 +88,10 @@ hipError_t launch_primary_ids(const DevScene& s, const CameraD& cam, int x0, int
                               int32_t* d_ids, hipStream_t stream);
 
 // Kernel variant: kernel 0 brute force, 1 grouped brute force, 2 BVH2 (24-entry stack), 3 wide BVH
-// (RT_WIDE_STACK = 40-entry stack), both + kStackOverflow entries in global memory;
+// (RT_WIDE_STACK = 16-entry stack), both + kStackOverflow entries in global memory;
 // lds stages the shading records in LDS.
 int path_variant(int kernel, bool lds);
-constexpr int kStackOverflow = 40; // = RT_STACK_OVF (kernels_path.hip)
+constexpr int kStackOverflow = 44; // = RT_STACK_OVF (kernels_path.hip)
 constexpr int kTestSpares = 3;     // zero TestRecs after the BVH-order records (leaf steps of up to 4 loads)
 int path_wide_stack();              // LDS entries of the wide BVH kernel's stack (RT_WIDE_STACK)
 size_t path_lds_bytes(const DevScene& s);   // dynamic LDS of the staged (lds) variants
@@ -108,6 +110,11 @@ int trace_rays_blocks_per_cu(int waves);
 int debug_vn_rehit(const double v0[3], const double e01[3], const double e02[3], int mirror, double u, double v,
                    const float dir[3], int* inside, double* t, double o[3]);
 hipError_t launch_trace_rays(const TraceRaysParams& p, int waves, int grid_blocks, hipStream_t stream);
+// The BVH order's rows (3 float4 per record, n_records including the spares) from its TestRecs and,
+// with rewrite, every homogeneous leaf reference of the BVH2 and the wide tree made compact
+// (rt_internal.h, kLeafCompact).
+hipError_t compact_leaves(const TestRec* d_tests, int n_records, float4* d_rows, NodeF* d_nodes, int n_nodes,
+                          Node4Q* d_nodes4, int n_nodes4, bool rewrite, hipStream_t stream);
 
 // partial -> fp64 planar accumulators (d_sum planes R | G | B, each `plane` doubles apart;
 // 0 = w*h), d_samples, d_misses (row-major w*h), added to.

@@ -133,6 +133,7 @@ struct rt_scene {
     struct {
         int builder = RT_BVH_BUILDER_HOST; // the one that ran
         int n_nodes2 = 0, n_nodes4 = 0, root2 = 0, root4 = 0, depth2 = 0, stack4 = 0, rounds = 0;
+        int leaves4 = 0, compact4 = 0; // leaf references of the wide tree, compact ones (kLeafCompact)
         float gpu_ms = 0.0f;
     } bvh;
     DevBuf<int32_t> order_d;      // GPU builder: primitive IDs in leaf order, planes appended
@@ -144,6 +145,7 @@ struct rt_scene {
     DevScene dev{};
     DevBuf<PrimF> prims_bf, prims_bvh;
     DevBuf<TestRec> tests_bf, tests_bvh;
+    DevBuf<float4> rows_bvh; // tests_bvh without the meta rows (compact leaves)
     DevBuf<RectRec> rects_bf;
     DevBuf<FrameRec> frames_bf;
     DevBuf<GroupRec> groups_bf;
@@ -1009,16 +1011,38 @@ int upload_scene(rt_scene* s)
                       (size_t)s->bvh.n_nodes2 * sizeof(NodeF) + (size_t)s->bvh.n_nodes4 * sizeof(Node4Q) +
                       xf.size() * sizeof(XformF) + mats.size() * sizeof(MatF) + vn.size() * sizeof(float4);
 
+    // Compact leaves: the BVH order's 48-B rows, and every leaf whose primitives share their kind and
+    // test flags referenced as a compact leaf (RTCORE_COMPACT_LEAVES=0 keeps them generic, for A/B)
+    {
+        const char* e = getenv("RTCORE_COMPACT_LEAVES");
+        const bool rewrite = !(e && e[0] == '0');
+        const size_t n_rec = n_bvh_records + kTestSpares;
+        HIP_TRY(s->rows_bvh.reserve(3 * n_rec));
+        HIP_TRY(compact_leaves(s->tests_bvh.p, (int)n_rec, s->rows_bvh.p, s->nodes.p, s->bvh.n_nodes2, s->nodes4.p,
+                               s->bvh.n_nodes4, rewrite, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+    }
     // Hot table: the first kHot wide nodes in breadth-first order from the root, their references
     // to each other rewritten to RT_HOT_BIT | hot index (the global tree is unchanged).
     std::vector<Node4Q> hot;
     int root4_hot = s->bvh.root4;
     {
-        int k_hot = 64; // with the 20-entry LDS stack: 6 blocks x (20 + 4) KB per CU
+        std::vector<Node4Q> all4((size_t)s->bvh.n_nodes4);
+        if (!all4.empty())
+            HIP_TRY(hipMemcpy(all4.data(), s->nodes4.p, all4.size() * sizeof(Node4Q), hipMemcpyDeviceToHost));
+        s->bvh.leaves4 = s->bvh.compact4 = 0; // build statistics: the wide tree's leaves, compact ones
+        for (const Node4Q& nd : all4)
+            for (float f : {nd.c.z, nd.c.w, nd.d.x, nd.d.y}) {
+                int32_t c;
+                std::memcpy(&c, &f, 4);
+                if (c < 0 && c != RT_NODE4_EMPTY) {
+                    s->bvh.leaves4++;
+                    s->bvh.compact4 += ((~c) & kLeafCompact) != 0;
+                }
+            }
+        int k_hot = 64; // with the 16-entry LDS stack: 7 blocks x (16 + 4) KB per CU
         if (const char* e = getenv("RTCORE_HOT_NODES")) k_hot = std::max(0, std::min(1024, atoi(e)));
         if (k_hot > 0 && s->bvh.root4 >= 0 && s->bvh.n_nodes4 > 0) {
-            std::vector<Node4Q> all4((size_t)s->bvh.n_nodes4);
-            HIP_TRY(hipMemcpy(all4.data(), s->nodes4.p, all4.size() * sizeof(Node4Q), hipMemcpyDeviceToHost));
             std::vector<int> order{s->bvh.root4};
             std::unordered_map<int, int> slot_of{{s->bvh.root4, 0}};
             for (size_t q = 0; q < order.size() && (int)order.size() < k_hot; q++) {
@@ -1059,6 +1083,7 @@ int upload_scene(rt_scene* s)
     d.root4_hot = root4_hot;
     d.tests_bf = s->tests_bf.p;
     d.tests_bvh = s->tests_bvh.p;
+    d.rows_bvh = s->rows_bvh.p;
     d.rects_bf = s->rects_bf.p;
     d.frames_bf = s->frames_bf.p;
     d.prims_bf = s->prims_bf.p;
@@ -1680,6 +1705,7 @@ int rt_debug_trace_rays(rt_scene* s, const void* d_rays, uint32_t n, void* d_hit
     p.counter = s->counter.p;
     p.stack_ovf = s->stack_ovf.p;
     p.tests = s->dev.tests_bvh;
+    p.rows = s->dev.rows_bvh;
     p.nodes4 = s->dev.nodes4;
     p.xf = s->dev.xf;
     p.root4 = s->dev.root4;
@@ -1744,7 +1770,8 @@ int rt_scene_get_build_stats(const rt_scene* s, double* out, int32_t n)
                                            (double)L.rects, (double)L.boxes, (double)L.frames, (double)L.frame_boxes,
                                            (double)L.frame_rects, (double)L.tris, (double)L.sphs,
                                            (double)s->dev.n_hot4, (double)s->jit.status, s->jit.compile_ms,
-                                           s->jit.from_cache ? 1.0 : 0.0, (double)L.group_max};
+                                           s->jit.from_cache ? 1.0 : 0.0, (double)L.group_max,
+                                           (double)s->bvh.leaves4, (double)s->bvh.compact4};
     for (int i = 0; i < n && i < RT_BUILD_STATS_COUNT; i++) out[i] = v[i];
     return RT_OK;
 }
@@ -1801,8 +1828,12 @@ int rt_scene_check_bvh(rt_scene* s)
         }
     std::string err;
     std::vector<int> seen(n, 0);
+    const uint32_t test_mask = KIND_MASK | F_MIRROR | F_TWOSIDED | F_INVERT | F_TRANSFORMED;
     auto leaf = [&](int ref, B& u) {
-        const int code = ~ref, first = code >> 3, cnt = (code & 7) + 1;
+        int first, cnt;
+        leaf_range(ref, first, cnt);
+        const bool compact = ((~ref) & kLeafCompact) != 0;
+        const uint32_t lfl = leaf_flags(((uint32_t)(~ref) >> 25) & 31u);
         if (first < 0 || first + cnt > nb) {
             err = "leaf range out of bounds";
             return;
@@ -1811,6 +1842,11 @@ int rt_scene_check_bvh(rt_scene* s)
             const int p = id[k];
             if (p < 0 || p >= n || H[p].kind == RT_PRIM_PLANE) {
                 err = "leaf record with a bad primitive ID";
+                return;
+            }
+            // a compact leaf's flags are what its primitives' own records say
+            if (compact && (H[p].flags & test_mask) != lfl) {
+                err = "compact leaf flags differ from primitive " + std::to_string(p);
                 return;
             }
             seen[p]++;

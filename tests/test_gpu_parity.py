@@ -309,6 +309,32 @@ def test_gpu_bvh_builder_renders(rc, scenes, name, mode):
     assert same > 0.99, same
 
 
+@pytest.mark.parametrize("builder", ["HOST", "GPU"])
+@pytest.mark.parametrize("name", ["MESH200", "SOUP", "bounce.txt"])
+def test_compact_leaves_render_identically(rc, scenes, name, builder, monkeypatch):
+    """Compact leaves (rt_internal.h kLeafCompact: the primitives' kind and test flags in the leaf
+    reference, 48-B records) render bit for bit what generic leaves (64-B records, flags per
+    record) render, through both trees and both builders.  The scenes mix triangles, spheres,
+    transformed spheres, one-sided, inverted and parallelogram faces, so that leaves of either kind
+    occur; rt_scene_check_bvh checks every compact leaf's flags against its primitives."""
+    scene = _builder_scene(rc, scenes, name)
+    b = getattr(rc, "RT_BVH_BUILDER_" + builder)
+    size = (64, 48)
+    for trav in (rc.RT_TRAVERSAL_BVH, rc.RT_TRAVERSAL_BVH2):
+        monkeypatch.setenv("RTCORE_COMPACT_LEAVES", "0")
+        g0 = rc.GpuRaytracer(scene, 0, size=size, traversal=trav, builder=b)
+        monkeypatch.delenv("RTCORE_COMPACT_LEAVES")
+        g1 = rc.GpuRaytracer(scene, 0, size=size, traversal=trav, builder=b)
+        st0, st1 = g0.build_stats(), g1.build_stats()
+        assert st0["compact_leaves"] == 0 and st1["wide_leaves"] == st0["wide_leaves"] > 0
+        assert st1["compact_leaves"] > 0.5 * st1["wide_leaves"], st1
+        g1.check_bvh()
+        r0 = g0.render_tile(0, 0, *size, 16, seed=6)
+        r1 = g1.render_tile(0, 0, *size, 16, seed=6)
+        for x, y in zip(r0, r1):
+            assert np.array_equal(x, y)
+
+
 def test_frame_multi_single_device(rc, scenes):
     """rt_render_frame_multi on one device equals a whole-frame tile render."""
     scene = scenes["die.txt"]
