@@ -1291,7 +1291,11 @@ PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint6
     // One device-scope atomic hands a wave p.pool items.  64 per atomic made the dispenser a
     // bottleneck (measured, 1080p: die.txt grouped 50.9 -> 47.0 ms with 256, 48.2 with 128 or 512;
     // bounce.txt flat 33.4 -> 33.0 ms with 128, 33.6 with 256; mesh BVH 82.2 -> 80.3 with 256).
-    int pool_mul = (s->variant >> 1) == 0 ? 2 : 4;
+    // With the XCD-local dispensers (8 words instead of one) smaller pools pay again (round 3, pool
+    // multiples 1 / 2 / 4 / 8): flat brute force C2 19.54-19.57 / 19.63-19.69 / 20.05 ms, the BVH
+    // kernels C4 44.54-44.57 / 44.25-44.28 / 45.0-45.2 / 46.8 ms; grouped C3 27.81 / - / 27.58-27.64.
+    const int kernel = s->variant >> 1;
+    int pool_mul = kernel == 0 ? 1 : kernel == 1 ? 4 : 2;
     if (const char* e = getenv("RTCORE_POOL_MUL")) pool_mul = std::max(1, std::min(64, atoi(e)));
     p.pool = 64;
     while (p.pool < 64 * pool_mul && p.pool < 64 * p.n_chunks) p.pool *= 2;

@@ -335,6 +335,23 @@ def test_compact_leaves_render_identically(rc, scenes, name, builder, monkeypatc
             assert np.array_equal(x, y)
 
 
+@pytest.mark.parametrize("name,mode", [("bounce.txt", "BRUTE"), ("die.txt", "GROUPED"), ("MESH200", "BVH")])
+def test_xcd_item_ranges_render_identically(rc, scenes, name, mode, monkeypatch):
+    """The XCD-local item ranges (8 dispensers, each strip of 8x8 blocks dealt first to one XCD's
+    workgroups, then stolen by the others) change which wave renders an item, never what the item
+    computes: a 256 x 160 frame (640 blocks, 8 ranges) renders bit for bit as with one dispenser,
+    and so does a tile too small to split (16 blocks)."""
+    scene = _builder_scene(rc, scenes, name)
+    g = rc.GpuRaytracer(scene, 0, size=(256, 160), traversal=getattr(rc, "RT_TRAVERSAL_" + mode))
+    for tile in ((0, 0, 256, 160), (40, 24, 32, 32)):
+        monkeypatch.setenv("RTCORE_XCD_SPLIT", "0")
+        a = g.render_tile(*tile, 8, seed=11)
+        monkeypatch.delenv("RTCORE_XCD_SPLIT")
+        b = g.render_tile(*tile, 8, seed=11)
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+
+
 def test_frame_multi_single_device(rc, scenes):
     """rt_render_frame_multi on one device equals a whole-frame tile render."""
     scene = scenes["die.txt"]
