@@ -584,11 +584,14 @@ __device__ __forceinline__ Ray3 camera_ray(const CamT& c, float x, float y)
 }
 
 // Raytracer.GetCameraRay (Raytracer.cs:262-282)
-template <class CamT>
+// LEAN (the brute-force kernels): x + U as one fma of the integer draw (U = h * 2^-24 exactly, so the
+// single rounding is the add's: the same value); the BVH kernels keep the add (their register
+// allocation moved spills into the traversal loop with it, C4 44.4 -> 55.9 ms)
+template <bool LEAN = false, class CamT>
 __device__ __forceinline__ void start_sample(const CamT& cam, int x, int y, Sample& S)
 {
-    const float sx = (float)x + next_u(S.rng);
-    const float sy = (float)y + next_u(S.rng);
+    const float sx = LEAN ? fmaf((float)rt_rng_next24(&S.rng), 0x1p-24f, (float)x) : (float)x + next_u(S.rng);
+    const float sy = LEAN ? fmaf((float)rt_rng_next24(&S.rng), 0x1p-24f, (float)y) : (float)y + next_u(S.rng);
     const Ray3 r = camera_ray(cam, sx, sy);
     S.o = r.o;
     S.d = r.d;
@@ -610,13 +613,16 @@ __device__ __forceinline__ void start_sample(const CamT& cam, int x, int y, Samp
     S.prev = -1;
 }
 
-// 1 - z^2 for z = 2^a (a <= 0) without cancellation: 1 - 2^(2a) = -expm1(2a ln 2); both forms
-// evaluated and selected (no divergent branch)
-__device__ __forceinline__ float one_minus_exp2_2a(float a)
+// 1 - z^2 for z = 2^a (a <= 0) without cancellation: 1 - 2^(2a) = -expm1(2a ln 2) by its series
+// near z = 1, else directly; both forms evaluated and selected (no divergent branch).  LEAN (the
+// brute-force kernels) takes the direct form as 1 - z z from the z already computed (z^2 <= 0.958
+// there, so the product's rounding costs a few ulp of the difference) instead of a second exp2.
+template <bool LEAN>
+__device__ __forceinline__ float one_minus_exp2_2a(float a, float z)
 {
     const float x = 2.0f * a * 0.69314718055994531f;
     const float series = -x * fmaf(x, fmaf(x, fmaf(x, 1.0f / 24.0f, 1.0f / 6.0f), 0.5f), 1.0f);
-    const float direct = 1.0f - __builtin_amdgcn_exp2f(2.0f * a);
+    const float direct = LEAN ? fmaf(-z, z, 1.0f) : 1.0f - __builtin_amdgcn_exp2f(2.0f * a);
     return x > -0.0625f ? series : direct;
 }
 
@@ -737,7 +743,7 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
     if (!(s.facts & FACT_INF_SHININESS) || !(__builtin_isinf(shin) && shin > 0.0f)) {
         const float a = __builtin_amdgcn_logf(next_u(S.rng)) * M.inv_shininess; // log2(U) / shininess
         z = __builtin_amdgcn_exp2f(a);
-        sz = fsqrt(one_minus_exp2_2a(a));
+        sz = fsqrt(one_minus_exp2_2a<!SLOT>(a, z));
     }
     const Frame fr = make_frame(nrm);
     const V3 rough = horizon(fr, nrm, z, sz, next_u(S.rng));
@@ -798,7 +804,11 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
         new_tint = transmit ? (inside ? v3(1.0f, 1.0f, 1.0f) : xyz(M.refraction)) : xyz(M.specular);
     }
     S.o = pos;
-    S.d = normalize(out_dir);
+    // the brute-force kernels do not renormalise, as the reference does not (new Ray(hit.Position,
+    // outDir), Raytracer.cs:186-218): the reflected, transmitted and CreateHorizon directions are
+    // unit vectors up to fp32 rounding.  The BVH kernels (SLOT) keep the normalisation (their
+    // register allocation moved spills into the traversal loop without it).
+    S.d = SLOT ? normalize(out_dir) : out_dir;
     S.prev = SLOT ? (b.sg >> 1) : id; // the BVH kernels name the left primitive by its slot
     if (VN && s.n_vn > 0 && kind == RT_PRIM_TRIANGLE && (fl & F_HASNORMALS)) {
         // does the reference's next query meet this triangle again (vn_rehit_test), and is that a
@@ -1014,7 +1024,7 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
         S.bounce = 0;
         S.prev = -1;
 #else
-        start_sample(cam, L.fx, L.fy, S);
+        start_sample<!NT>(cam, L.fx, L.fy, S);
 #endif
         L.live = true;
     }
