@@ -211,6 +211,48 @@ __device__ __forceinline__ void rect_group(RectP r, int n, V3 o, V3 d, V3 id, V3
 #endif
 }
 
+// Min / max as the bare VALU instructions.  fminf / fmaxf of values the compiler cannot prove
+// canonical (here: slab distances that pass through the sphere tests' divergent branches) get a
+// v_max_f32 x, x, x quieting each operand first; our operands are never signalling NaNs, and a
+// quiet NaN operand is ignored either way (IEEE minNum), so the bare instruction is the same min.
+__device__ __forceinline__ float vmin(float a, float b)
+{
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float vmax(float a, float b)
+{
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+__device__ __forceinline__ float vmax3(float a, float b, float c)
+{
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float vmin3(float a, float b, float c)
+{
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float vmax0(float a)
+{
+    float r;
+    asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(a));
+    return r;
+}
+__device__ __forceinline__ float vmax1(float a)
+{
+    float r;
+    asm("v_max_f32 %0, 1.0, %1" : "=v"(r) : "v"(a));
+    return r;
+}
+
 // Closed box (BoxRec): one slab test gives the entry and exit distances and faces; each is a
 // hit when it lies in [0, best), its face keeps hits from that side (culling) and it is not the
 // face the ray leaves (self-hit).  The entry wins when both are hits.  Equivalent to testing the
@@ -225,9 +267,9 @@ __device__ __forceinline__ void hit_box(const BoxRec& B, V3 o, V3 d, V3 id, V3 o
     const float hy = SUB ? (B.hi.y - oi.y) * id.y : fmaf(B.hi.y, id.y, -oi.y);
     const float lz = SUB ? (B.lo.z - oi.z) * id.z : fmaf(B.lo.z, id.z, -oi.z);
     const float hz = SUB ? (B.hi.z - oi.z) * id.z : fmaf(B.hi.z, id.z, -oi.z);
-    const float nx = fminf(lx, hx), ny = fminf(ly, hy), nz = fminf(lz, hz);
-    const float fx = fmaxf(lx, hx), fy = fmaxf(ly, hy), fz = fmaxf(lz, hz);
-    const float te = fmaxf(fmaxf(nx, ny), nz), tx = fminf(fminf(fx, fy), fz);
+    const float nx = vmin(lx, hx), ny = vmin(ly, hy), nz = vmin(lz, hz);
+    const float fx = vmax(lx, hx), fy = vmax(ly, hy), fz = vmax(lz, hz);
+    const float te = vmax3(nx, ny, nz), tx = vmin3(fx, fy, fz);
     const bool meet = te <= tx;
     // the ray enters axis a's slab by its lower plane (side 0) when d[a] > 0
     const int sx = (int)(__float_as_uint(d.x) >> 31), sy = (int)(__float_as_uint(d.y) >> 31),
@@ -261,15 +303,30 @@ __device__ __forceinline__ float slab_rcp(float d)
 {
     return rcp(fabsf(d) >= 5.421010862e-20f ? d : __builtin_copysignf(5.421010862e-20f, d));
 }
+// The brute-force kernels' form: the reciprocal clamped to +-2^64 by one v_med3 instead of a
+// compare, a select and a sign insert before it; the same value for every finite or zero d
+// (1/(+-0) = +-inf clamps to +-2^64 = 1/(+-2^-64)).  (A NaN d, from a vertex-normal triangle's NaN
+// normal, gets -2^64 instead of 2^64 with the NaN's sign: its rectangle, triangle and sphere tests
+// fail either way.)
+__device__ __forceinline__ float slab_rcp_lean(float d)
+{
+    return __builtin_amdgcn_fmed3f(rcp(d), -0x1p64f, 0x1p64f);
+}
 
+// BARE (the brute-force kernels' group boxes): the per-axis min / max as bare instructions (vmin,
+// vmax), which drops the compiler's NaN quieting of their operands; same values.
+template <bool BARE = false>
 __device__ __forceinline__ bool slab(float4 lo, float4 hi, V3 oi, V3 id, float tmax, float& tnear)
 {
     // t = box * (1/d) - o * (1/d); NaN from 0*inf is ignored by fminf/fmaxf (conservative)
     const float tx0 = fmaf(lo.x, id.x, -oi.x), tx1 = fmaf(hi.x, id.x, -oi.x);
     const float ty0 = fmaf(lo.y, id.y, -oi.y), ty1 = fmaf(hi.y, id.y, -oi.y);
     const float tz0 = fmaf(lo.z, id.z, -oi.z), tz1 = fmaf(hi.z, id.z, -oi.z);
-    const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-    const float tmx = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    const float nx = BARE ? vmin(tx0, tx1) : fminf(tx0, tx1), fx = BARE ? vmax(tx0, tx1) : fmaxf(tx0, tx1);
+    const float ny = BARE ? vmin(ty0, ty1) : fminf(ty0, ty1), fy = BARE ? vmax(ty0, ty1) : fmaxf(ty0, ty1);
+    const float nz = BARE ? vmin(tz0, tz1) : fminf(tz0, tz1), fz = BARE ? vmax(tz0, tz1) : fmaxf(tz0, tz1);
+    const float tmin = BARE ? vmax3(nx, ny, vmax0(nz)) : fmaxf(fmaxf(nx, ny), fmaxf(nz, 0.0f));
+    const float tmx = BARE ? vmin3(fx, fy, vmin(fz, tmax)) : fminf(fminf(fx, fy), fminf(fz, tmax));
     tnear = tmin;
     return tmin <= tmx * 1.00000024f;
 }
@@ -284,7 +341,7 @@ __device__ __forceinline__ void trace_brute(const SceneT& s, GroupP groups, Test
                                             BoxP boxes, XfP xf, V3 o, V3 d, int prev, Best& b, unsigned& n_flat,
                                             unsigned& n_sph, unsigned& n_node)
 {
-    const V3 id = v3(slab_rcp(d.x), slab_rcp(d.y), slab_rcp(d.z));
+    const V3 id = v3(slab_rcp_lean(d.x), slab_rcp_lean(d.y), slab_rcp_lean(d.z));
     const V3 oi = o * id;
     const int n_groups = CULL ? s.n_groups : 1; // the flat order is one group (1/d and o/d die after its rects)
 #ifdef RT_SCENE_CONST
@@ -295,7 +352,7 @@ __device__ __forceinline__ void trace_brute(const SceneT& s, GroupP groups, Test
         if (CULL) {
             if (STATS) n_node++; // the group's box: a node of a one-level tree (SURVEY 8(d) N_node)
             float tn;
-            if (!__any(slab(G.lo, G.hi, oi, id, b.t, tn))) continue;
+            if (!__any(slab<true>(G.lo, G.hi, oi, id, b.t, tn))) continue;
         }
         if (STATS) { // primitive tests actually made (groups the wave skipped are not counted)
             n_flat += G.n_rect[0] + G.n_rect[1] + G.n_rect[2] + G.n_flat_extra + (G.n_tri_sph & 0xFFFF);
@@ -752,7 +809,11 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
     float spec_lum = M.specular.w, refr_lum = M.refraction.w;
     const float cs = -dot(rough, S.d);
     float cos_out = 0.0f, ior_ratio = 0.0f;
-    if ((s.facts & FACT_IOR) && ((refr_lum > 0.0f) | (spec_lum > 0.0f)) && M.ior != 0.0f &&
+    // (luminances are never NaN: for them x > 0 is the integer compare of the bits, which needs no
+    // quieting of the LDS-loaded operands as the max the compiler made of the float form did)
+    const bool some_lum = SLOT ? ((refr_lum > 0.0f) | (spec_lum > 0.0f))
+                               : ((__float_as_int(refr_lum) > 0) | (__float_as_int(spec_lum) > 0));
+    if ((s.facts & FACT_IOR) && some_lum && M.ior != 0.0f &&
         cs >= 0.0f) { // Raytracer.cs:120-161
         ior_ratio = inside ? M.eta_exit : M.eta_enter; // eta = iorIn / iorOut
         const float sin_out = ior_ratio * fsqrt(1.0f - cs * cs);
@@ -823,7 +884,7 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
                 S.prev = -2 - ((b.sg & ~1) | (int)gin2);
         }
     }
-    S.tint = S.tint * (new_tint * fmaxf(total, 1.0f));
+    S.tint = S.tint * (new_tint * (SLOT ? fmaxf(total, 1.0f) : vmax1(total)));
     S.bounce++;
     return 0;
 }
