@@ -1059,8 +1059,12 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
 #else
                     // the frame width from the launch record (a scene-specialised build's constant
                     // scene leaves it out, so one build serves every frame size)
-                    L.pkey = rt_rng_pixel_key(p.seed_key, (unsigned long long)L.fy * (unsigned long long)p.scene.width +
-                                                              (unsigned long long)L.fx);
+                    const unsigned long long px =
+                        (unsigned long long)L.fy * (unsigned long long)p.scene.width + (unsigned long long)L.fx;
+                    // the brute-force kernels read the key from the scene's table (the same value:
+                    // two hash rounds fewer per item open, which runs in most iterations)
+                    if (!NT && p.pkeys) L.pkey = p.pkeys[px];
+                    else L.pkey = rt_rng_pixel_key(p.seed_key, px);
 #endif
                 }
             }
@@ -2044,6 +2048,21 @@ hipError_t compact_leaves(const TestRec* d_tests, int n_records, float4* d_rows,
     if (rewrite && n > 0)
         hipLaunchKernelGGL(compact_nodes_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_nodes, n_nodes, d_nodes4,
                            n_nodes4, d_tests);
+    return hipGetLastError();
+}
+
+__global__ void pixel_keys_kernel(rt_key2 seed_key, int w, int h, rt_key2* __restrict__ out)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)w * (size_t)h) return;
+    out[i] = rt_rng_pixel_key(seed_key, (unsigned long long)i);
+}
+
+hipError_t launch_pixel_keys(rt_key2 seed_key, int w, int h, rt_key2* out, hipStream_t stream)
+{
+    const size_t n = (size_t)w * (size_t)h;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(pixel_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, seed_key, w, h, out);
     return hipGetLastError();
 }
 

@@ -31,6 +31,8 @@ struct PathParams {
     unsigned long long seed;
     rt_key2 seed_key;           // rt_rng_seed_key(seed) (rtcore_rng.h)
     unsigned long long sample_base;
+    const rt_key2* pkeys;       // brute-force kernels: rt_rng_pixel_key(seed_key, pixel) per frame pixel
+                                // (cached per scene and seed, pixel_keys_kernel), or null: hashed per item
     unsigned int* counter;      // work-item dispensers (zeroed before launch), one per item range, kSplitStride apart
     int n_split;                // item ranges (1 or kMaxSplit): range g = blocks [split_start[g], split_start[g + 1])
                                 // in item units, dealt first to the workgroups b with b % n_split == g (the
@@ -110,6 +112,8 @@ int trace_rays_blocks_per_cu(int waves);
 int debug_vn_rehit(const double v0[3], const double e01[3], const double e02[3], int mirror, double u, double v,
                    const float dir[3], int* inside, double* t, double o[3]);
 hipError_t launch_trace_rays(const TraceRaysParams& p, int waves, int grid_blocks, hipStream_t stream);
+// out[y * w + x] = rt_rng_pixel_key(seed_key, y * w + x) for a w x h frame
+hipError_t launch_pixel_keys(rt_key2 seed_key, int w, int h, rt_key2* out, hipStream_t stream);
 // The BVH order's rows (3 float4 per record, n_records including the spares) from its TestRecs and,
 // with rewrite, every homogeneous leaf reference of the BVH2 and the wide tree made compact
 // (rt_internal.h, kLeafCompact).

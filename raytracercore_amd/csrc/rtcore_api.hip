@@ -186,6 +186,9 @@ struct rt_scene {
     DevBuf<RefNode> ref_nodes;
     // work buffers
     DevBuf<unsigned int> counter;
+    DevBuf<rt_key2> pkeys;       // pixel-key table of the brute-force kernels (PathParams::pkeys)
+    bool pkeys_valid = false;
+    uint64_t pkeys_seed = 0;
     DevBuf<int> stack_ovf;
     DevBuf<unsigned long long> rays;
     DevBuf<float4> partial;
@@ -1457,6 +1460,21 @@ int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t
         HIP_TRY(s->params_d.reserve(rt_scene::kParamRing));
     }
     fill_launch(s->dev, s->variant, p);
+    // The brute-force kernels read each item's pixel key (two lowbias32 rounds of the seed key and
+    // the frame pixel index, rtcore_rng.h) from a per-scene table, built here once per seed (a
+    // ~10-us kernel on the launch stream): the same keys, without hashing in the loop.
+    // RTCORE_PIXEL_KEYS=0 hashes per item (A/B).
+    p.pkeys = nullptr;
+    static const bool pkeys_on = !(getenv("RTCORE_PIXEL_KEYS") && getenv("RTCORE_PIXEL_KEYS")[0] == '0');
+    if ((s->variant >> 1) < 2 && !s->stats_on && pkeys_on) {
+        if (!s->pkeys_valid || s->pkeys_seed != p.seed) {
+            HIP_TRY(s->pkeys.reserve((size_t)s->params.width * (size_t)s->params.height));
+            HIP_TRY(launch_pixel_keys(p.seed_key, s->params.width, s->params.height, s->pkeys.p, stream));
+            s->pkeys_valid = true;
+            s->pkeys_seed = p.seed;
+        }
+        p.pkeys = s->pkeys.p;
+    }
     const unsigned slot = s->params_next++ % rt_scene::kParamRing;
     hipEvent_t& sev = s->slot_ev[slot];
     if (sev) HIP_TRY(hipEventSynchronize(sev)); // the slot's previous upload has been read
