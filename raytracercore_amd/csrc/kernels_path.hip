@@ -46,7 +46,7 @@ __device__ __forceinline__ float dot(V3 a, V3 b) { return fmaf(a.x, b.x, fmaf(a.
 // computes the same values except for the sign of an exact zero (x is always finite here).
 __device__ __forceinline__ bool known_zero(float c)
 {
-#if defined(RT_SCENE_CONST) && !defined(RT_EXP_NO_KFOLD)
+#if defined(RT_SCENE_CONST)
     return __builtin_constant_p(c) && c == 0.0f;
 #else
     (void)c;
@@ -184,16 +184,6 @@ __device__ __forceinline__ void hit_rect(const RectRec& R, int sg, V3 o, V3 d, V
 template <int AXIS, bool SUB = false, class RectP>
 __device__ __forceinline__ void rect_group(RectP r, int n, V3 o, V3 d, V3 id, V3 oi, int prev, Best& b)
 {
-#ifdef RT_EXP_RECT_UNROLL4
-    for (; n >= 4; n -= 4, r += 4) {
-        const RectRec r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
-        hit_rect<AXIS, SUB>(r0, r0.sg, o, d, id, oi, prev, b);
-        hit_rect<AXIS, SUB>(r1, r1.sg, o, d, id, oi, prev, b);
-        hit_rect<AXIS, SUB>(r2, r2.sg, o, d, id, oi, prev, b);
-        hit_rect<AXIS, SUB>(r3, r3.sg, o, d, id, oi, prev, b);
-    }
-#endif
-#ifndef RT_EXP_RECT_NO_UNROLL
     for (; n >= 2; n -= 2, r += 2) {
         const RectRec r0 = r[0], r1 = r[1];
         hit_rect<AXIS, SUB>(r0, r0.sg, o, d, id, oi, prev, b);
@@ -203,12 +193,6 @@ __device__ __forceinline__ void rect_group(RectP r, int n, V3 o, V3 d, V3 id, V3
         const RectRec r0 = r[0];
         hit_rect<AXIS, SUB>(r0, r0.sg, o, d, id, oi, prev, b);
     }
-#else
-    for (; n > 0; n--, r++) {
-        const RectRec r0 = r[0];
-        hit_rect<AXIS, SUB>(r0, r0.sg, o, d, id, oi, prev, b);
-    }
-#endif
 }
 
 // Min / max as the bare VALU instructions.  fminf / fmaxf of values the compiler cannot prove
@@ -305,9 +289,9 @@ __device__ __forceinline__ float slab_rcp(float d)
 }
 // The brute-force kernels' form: the reciprocal clamped to +-2^64 by one v_med3 instead of a
 // compare, a select and a sign insert before it; the same value for every finite or zero d
-// (1/(+-0) = +-inf clamps to +-2^64 = 1/(+-2^-64)).  (A NaN d, from a vertex-normal triangle's NaN
-// normal, gets -2^64 instead of 2^64 with the NaN's sign: its rectangle, triangle and sphere tests
-// fail either way.)
+// (1/(+-0) = +-inf clamps to +-2^64 = 1/(+-2^-64)).  A NaN d (a vertex-normal triangle's NaN
+// normal) gets a finite +-2^64 here, so a box test could report a hit for it: path_body ends such
+// a query as a miss, as the reference's BVH root test does.
 __device__ __forceinline__ float slab_rcp_lean(float d)
 {
     return __builtin_amdgcn_fmed3f(rcp(d), -0x1p64f, 0x1p64f);
@@ -370,7 +354,6 @@ __device__ __forceinline__ void trace_brute(const SceneT& s, GroupP groups, Test
         }
         // rectangles in a common affine frame: the ray mapped once, then the same rect tests (t is
         // invariant under the map; a local d of 0 gives an infinite or NaN t, which never hits)
-#ifndef RT_EXP_NO_FRAMES
         for (int f = G.frame_first; f < G.frame_first + G.n_frames; f++) {
             const FrameRec F = frames[f];
             const V3 lo = v3(dot4(F.r0, o), dot4(F.r1, o), dot4(F.r2, o));
@@ -387,7 +370,6 @@ __device__ __forceinline__ void trace_brute(const SceneT& s, GroupP groups, Test
                 hit_box<true>(B, lo, ld, lid, lo, prev, b);
             }
         }
-#endif
         int i = __float_as_int(G.hi.w);
         int end = i + (G.n_tri_sph & 0xFFFF);
         if (i < end) {
@@ -623,11 +605,33 @@ __device__ __forceinline__ float acos_turn2(float u)
 struct Ray3 {
     V3 o, d;
 };
+// The camera's kind and depth-of-field switch: compile-time constants in a camera-independent
+// scene-specialised build (rt_jit.cpp), else read from the camera record.
+template <class CamT>
+__device__ __forceinline__ bool cam_frustum(const CamT& c)
+{
+#ifdef RT_SCENE_CAMERA_KIND
+    (void)c;
+    return RT_SCENE_CAMERA_KIND == RT_CAMERA_FRUSTUM;
+#else
+    return c.kind == RT_CAMERA_FRUSTUM;
+#endif
+}
+template <class CamT>
+__device__ __forceinline__ bool cam_dof(const CamT& c)
+{
+#ifdef RT_SCENE_CAMERA_DOF
+    (void)c;
+    return RT_SCENE_CAMERA_DOF != 0;
+#else
+    return c.dof != 0.0f;
+#endif
+}
 template <class CamT> // CameraF, or CameraF in the constant address space (scalar loads)
 __device__ __forceinline__ Ray3 camera_ray(const CamT& c, float x, float y)
 {
     Ray3 r;
-    if (c.kind == RT_CAMERA_FRUSTUM) {
+    if (cam_frustum(c)) {
         const float ox = fmaf(x, c.tan_x_per_px, -c.tan_x); // tan_x * (x - w2) / w2
         const float oy = fmaf(y, c.tan_y_per_px, -c.tan_y);
         r.d = normalize(madd(xyz(c.up), oy, madd(xyz(c.side), ox, xyz(c.look))));
@@ -652,11 +656,7 @@ __device__ __forceinline__ void start_sample(const CamT& cam, int x, int y, Samp
     const Ray3 r = camera_ray(cam, sx, sy);
     S.o = r.o;
     S.d = r.d;
-#ifdef RT_EXP_NO_DOF
-    if (false) {
-#else
-    if (cam.dof != 0.0f) {
-#endif
+    if (cam_dof(cam)) {
         const V3 focus = madd(r.d, cam.focal_length - cam.image_plane, r.o);
         const float dist = fsqrt(next_u(S.rng)) * cam.dof;
         const float turn = next_u(S.rng);
@@ -724,6 +724,17 @@ __host__ __device__ __noinline__ bool vn_rehit_test(const PrimD& P, double u, do
         o_out[2] = o[2];
     }
     return !rej;
+}
+
+// Raytracer.cs:74-75: `if (i % 3 == 0) ray = Ray.Directional(...)` at the start of bounce i.  Here
+// i <= Recursion; for the (usual) recursion depths below 32 the brute-force kernels test one bit of a
+// constant.  The BVH kernels (SLOT) take the plain remainder: the bit test's extra scene read moved
+// their register spills (C4 wide kernel 17 -> 23 VGPRs spilled).
+template <bool SLOT, class SceneT>
+__device__ __forceinline__ bool renormalise_at(const SceneT& s, int i)
+{
+    if (SLOT) return (unsigned)i % 3u == 0u;
+    return s.recursion < 32 ? ((0x49249249u >> (unsigned)i) & 1u) != 0 : (unsigned)i % 3u == 0u;
 }
 
 // The closest hit a query starts from: none, or the re-hit of a vertex-normal triangle that
@@ -865,11 +876,12 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
         new_tint = transmit ? (inside ? v3(1.0f, 1.0f, 1.0f) : xyz(M.refraction)) : xyz(M.specular);
     }
     S.o = pos;
-    // the brute-force kernels do not renormalise, as the reference does not (new Ray(hit.Position,
-    // outDir), Raytracer.cs:186-218): the reflected, transmitted and CreateHorizon directions are
-    // unit vectors up to fp32 rounding.  The BVH kernels (SLOT) keep the normalisation (their
-    // register allocation moved spills into the traversal loop without it).
-    S.d = SLOT ? normalize(out_dir) : out_dir;
+    // GetColor renormalises the direction at the start of bounces i = 0, 3, 6, 9, ... only
+    // (Raytracer.cs:74-75, Ray.Directional); the ray leaving this bounce is traced as bounce
+    // S.bounce + 1.  The reflected, transmitted and CreateHorizon directions are unit vectors up to
+    // rounding, so one Newton step of 1/|d| (1.5 - 0.5 |d|^2, relative error (|d|^2 - 1)^2) is the
+    // normalisation to fp32 precision, without the reciprocal square root.
+    S.d = out_dir * (renormalise_at<SLOT>(s, S.bounce + 1) ? fmaf(-0.5f, dot(out_dir, out_dir), 1.5f) : 1.0f);
     S.prev = SLOT ? (b.sg >> 1) : id; // the BVH kernels name the left primitive by its slot
     if (VN && s.n_vn > 0 && kind == RT_PRIM_TRIANGLE && (fl & F_HASNORMALS)) {
         // does the reference's next query meet this triangle again (vn_rehit_test), and is that a
@@ -1054,9 +1066,6 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
                         }
                         L.fy = p.y0 + ((int)bq * p.band_stride + p.band_offset) * p.band + (int)br;
                     }
-#ifdef RT_EXP_CHEAP_PKEY // cost experiment: no pixel-key hashing
-                    L.pkey = rt_key2{(unsigned)L.fx * 0x9E3779B9u, (unsigned)L.fy};
-#else
                     // the frame width from the launch record (a scene-specialised build's constant
                     // scene leaves it out, so one build serves every frame size)
                     const unsigned long long px =
@@ -1065,7 +1074,6 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
                     // two hash rounds fewer per item open, which runs in most iterations)
                     if (!NT && p.pkeys) L.pkey = p.pkeys[px];
                     else L.pkey = rt_rng_pixel_key(p.seed_key, px);
-#endif
                 }
             }
         }
@@ -1077,20 +1085,8 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
         }
     }
     if (L.active && L.item_open && !L.live && L.cnt >= 65536u) {
-#ifdef RT_EXP_CHEAP_SKEY // cost experiment: no sample-key hashing
-        S.rng = rt_rng{L.pkey.a + (unsigned)L.s_next * 0x85EBCA6Bu, L.pkey.b};
-#else
         S.rng = rt_rng_from_pixel_key(L.pkey, p.sample_base + (unsigned long long)L.s_next);
-#endif
-#ifdef RT_EXP_CHEAP_CAMERA // cost experiment: a fixed camera ray per pixel (no draws, no normalise)
-        S.o = xyz(cam.position);
-        S.d = v3(cam.look.x + (float)L.fx * 1e-4f, cam.look.y + (float)L.fy * 1e-4f, cam.look.z);
-        S.tint = v3(1.0f, 1.0f, 1.0f);
-        S.bounce = 0;
-        S.prev = -1;
-#else
         start_sample<!NT>(cam, L.fx, L.fy, S);
-#endif
         L.live = true;
     }
 }
@@ -1191,7 +1187,6 @@ __device__ __forceinline__ void path_body(const CameraF* __restrict__ camp, cons
     S.bounce = 0;
     Counters cnt{};
     unsigned long long wave_rays = 0; // wave-uniform
-    float exp_sink = 0.0f; // keeps the cost-experiment work alive (RT_EXP_*)
 
     while (true) {
         unsigned long long t0 = 0, t1 = 0, t2 = 0;
@@ -1210,21 +1205,13 @@ __device__ __forceinline__ void path_body(const CameraF* __restrict__ camp, cons
 #else
         const auto& sc = pq->scene;
 #endif
-#ifdef RT_SCENE_CONST
+#if defined(RT_SCENE_CONST) && RT_SCENE_CONST_CAMERA
         refill<false>(L, S, *pq, sc, *(const CameraF*)kCameraW, lane, total); // the camera compiled in too
 #else
         refill<false>(L, S, *pq, sc, *cp, lane, total);
 #endif
         if (!__any(L.active)) break;
         if (STATS) t1 = __builtin_readcyclecounter();
-#ifdef RT_EXP_DUP_START // cost experiment: a second camera sample on a copy
-        if (L.live) {
-            Sample S2 = S;
-            S2.rng.k0 ^= (unsigned)S.bounce;
-            start_sample(*cp, L.fx, L.fy, S2);
-            exp_sink += S2.o.x + S2.d.y;
-        }
-#endif
         wave_rays += (unsigned)__popcll(__ballot(L.live)); // one Scene.RayTrace per live lane
         if (L.live) {
 #ifdef RT_SCENE_CONST // scene-specialised build (rt_jit.cpp): the records are compile-time constants
@@ -1244,34 +1231,20 @@ __device__ __forceinline__ void path_body(const CameraF* __restrict__ camp, cons
 #endif
             const auto vnormals = (const RT_AS_CONST float4*)pq->vnormals;
             Best b = query_start<VN>(sc, S.prev);
-#ifdef RT_EXP_DUP_TRACE // cost experiment: a second closest-hit query from a perturbed origin
-            {
-                Best b2{__builtin_huge_valf(), -1};
-                unsigned u0 = 0, u1 = 0, u2 = 0;
-                trace_brute<CULL, false>(sc, groups, tests, rects, frames, boxes, xf,
-                                         S.o + v3(exp_sink * 1e-30f, 0, 0), S.d, S.prev, b2, u0, u1, u2);
-                exp_sink += b2.t;
-            }
-#endif
-#ifndef RT_EXP_NO_TRACE // cost experiment: every camera ray misses (per-sample overhead alone)
             trace_brute<CULL, STATS>(sc, groups, tests, rects, frames, boxes, xf, S.o, S.d, S.prev, b, cnt.tris,
                                      cnt.sphs, cnt.nodes);
-#endif
             const int pln0 = sc.n_bvh;
             for (int i = pln0; i < pln0 + sc.n_pln; i++) {
                 const TestRec tr = tests[i];
                 hit_plane(tr, i, S.o, S.d, S.prev, b);
             }
+            // A NaN direction (a diffuse bounce about GetNormal's NaN normal, only in scenes with
+            // vertex-normal triangles) fails the reference's BVH root test (BVH.cs:301-303: far >= 0
+            // is false for NaN) and meets nothing.  The brute-force records would not all say so: a
+            // box's slab reciprocals stay finite for NaN (slab_rcp_lean), so a NaN ray inside a room
+            // box met its exit face.
+            if (VN && __builtin_isnan(S.d.x + S.d.y + S.d.z)) b = Best{__builtin_huge_valf(), -1};
             if (STATS) t2 = __builtin_readcyclecounter();
-#ifdef RT_EXP_DUP_SHADE // cost experiment: a second bounce on a copy
-            {
-                Sample S2 = S;
-                S2.rng.k0 ^= (unsigned)S.bounce;
-                V3 c2;
-                shade<VN>(sc, R.prims, R.mats, R.xfs, vnormals, tests, pq->prims_d, b, S2, c2);
-                exp_sink += c2.x + S2.d.x;
-            }
-#endif
             bounce<VN>(L, S, sc, R, vnormals, tests, pq->prims_d, b);
         } else if (STATS) {
             t2 = __builtin_readcyclecounter();
@@ -1284,7 +1257,6 @@ __device__ __forceinline__ void path_body(const CameraF* __restrict__ camp, cons
             cnt.iters++;
         }
     }
-    if (exp_sink == 1234.5f) pp->partial[0].x = exp_sink;
     flush_counts<STATS>(wave_rays, cnt, *(const ParamsC*)pp, lane);
 }
 
@@ -1781,15 +1753,17 @@ __global__ void rows_kernel(const TestRec* __restrict__ tests, int n, float4* __
     rows[3 * (size_t)i + 2] = t.r2;
 }
 
-// A generic leaf whose primitives (at most 4, from slot < 2^23) share their kind (triangle or sphere)
-// and test flags becomes a compact leaf; any other reference is returned unchanged.
+// A generic leaf whose primitives (at most 4, all of them at slots below 2^23) share their kind
+// (triangle or sphere) and test flags becomes a compact leaf; any other reference is returned
+// unchanged.  (A leaf reaching past slot 2^23 stays generic: leaf_advance adds to the first-slot
+// field, whose carry would run into the flag bits.)
 __device__ int compact_ref(int ref, const TestRec* __restrict__ tests)
 {
     if (ref >= 0 || ref == RT_NODE4_EMPTY) return ref;
     const int code = ~ref;
     if (code & kLeafCompact) return ref;
     const int first = code >> 3, count = (code & 7) + 1;
-    if (count > 4 || first >= kLeafCompactMaxFirst) return ref;
+    if (count > 4 || first + count > kLeafCompactMaxFirst) return ref;
     uint32_t key = 0;
     for (int j = 0; j < count; j++) {
         const uint32_t fl = __float_as_uint(tests[first + j].meta.y), kind = fl & KIND_MASK;

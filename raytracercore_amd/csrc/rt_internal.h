@@ -199,6 +199,7 @@ struct PathScene {
 // generic leaves; compact_leaves (kernels_path.hip) rewrites every homogeneous one after the upload.
 constexpr int kLeafCompact = 1 << 30;
 constexpr int kLeafCompactMaxFirst = 1 << 23;
+constexpr int kLeafGenericMaxSlots = 1 << 27; // slots a generic leaf code can address (rt_scene_create refuses more)
 __host__ __device__ inline void leaf_range(int ref, int& first, int& count)
 {
     const int code = ~ref;

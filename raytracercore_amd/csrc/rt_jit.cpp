@@ -117,7 +117,7 @@ void write_file_atomic(const std::string& dir, const std::string& path, const st
     prune_cache(dir);
 }
 
-// RTCORE_JIT_FLAGS: extra compiler flags for experiments (e.g. "-DRT_EXP_DUP_TRACE"), space-separated
+// RTCORE_JIT_FLAGS: extra compiler flags for experiments (e.g. "-DRT_PATH_WAVES=8"), space-separated
 std::vector<std::string> jit_extra_flags()
 {
     std::vector<std::string> out;
@@ -231,7 +231,7 @@ bool jit_enabled()
 
 void jit_set_enabled(bool on) { g_jit.store(on ? 1 : 0); }
 
-std::string jit_scene_header(const PathScene& ps, const CameraF& cam, const std::vector<GroupRec>& groups,
+std::string jit_scene_header(const PathScene& ps, const CameraF& cam, bool with_camera, const std::vector<GroupRec>& groups,
                              const std::vector<RectRec>& rects, const std::vector<FrameRec>& frames,
                              const std::vector<TestRec>& tests, const std::vector<XformF>& xf)
 {
@@ -243,7 +243,13 @@ std::string jit_scene_header(const PathScene& ps, const CameraF& cam, const std:
     p.n_hot4 = 0;
     p.width = 0;      // read from the launch record (one build serves every frame size)
     put_words(o, "kSceneW", std::vector<PathScene>{p});
-    put_words(o, "kCameraW", std::vector<CameraF>{cam});
+    if (with_camera) {
+        o << "#define RT_SCENE_CONST_CAMERA 1\n";
+        put_words(o, "kCameraW", std::vector<CameraF>{cam});
+    } else { // camera-independent: its kind and depth-of-field switch only
+        o << "#define RT_SCENE_CONST_CAMERA 0\n#define RT_SCENE_CAMERA_KIND " << cam.kind
+          << "\n#define RT_SCENE_CAMERA_DOF " << (cam.dof != 0.0f ? 1 : 0) << "\n";
+    }
     put_words(o, "kGroupsW", groups);
     put_words(o, "kRectsW", rects);
     put_words(o, "kFramesW", frames);
@@ -354,7 +360,7 @@ void jit_release(int device, hipFunction_t fn)
 
 size_t jit_compile_check(const std::string& arch, bool grouped, std::string& err)
 {
-    const std::string header = jit_scene_header(PathScene{}, CameraF{}, {}, {}, {}, {}, {});
+    const std::string header = jit_scene_header(PathScene{}, CameraF{}, grouped, {}, {}, {}, {}, {});
     std::vector<char> code;
     if (!compile(arch, main_source(grouped), header, code, err)) return 0;
     return code.size();

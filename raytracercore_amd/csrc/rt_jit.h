@@ -15,9 +15,12 @@
 
 namespace rtc {
 
-// The generated header (kSceneW, kCameraW, kGroupsW, kRectsW, kFramesW, kTestsW, kXfW) of one
-// scene, camera and slot order.
-std::string jit_scene_header(const PathScene& ps, const CameraF& cam, const std::vector<GroupRec>& groups,
+// The generated header (kSceneW, kGroupsW, kRectsW, kFramesW, kTestsW, kXfW) of one scene and
+// slot order.  with_camera: the camera's values as well (kCameraW; the grouped order, whose group
+// order is per camera anyway); otherwise only its kind and whether it has depth of field are
+// compiled in (RT_SCENE_CAMERA_KIND, RT_SCENE_CAMERA_DOF) and the kernel reads the camera from
+// device memory, so one build serves every camera of those two facts.
+std::string jit_scene_header(const PathScene& ps, const CameraF& cam, bool with_camera, const std::vector<GroupRec>& groups,
                              const std::vector<RectRec>& rects, const std::vector<FrameRec>& frames,
                              const std::vector<TestRec>& tests, const std::vector<XformF>& xf);
 

@@ -173,6 +173,7 @@ struct rt_scene {
         double compile_ms = 0;
         bool from_cache = false;
         std::string error;
+        std::string header;        // the generated scene header fn was built from
     } jit;
     double grouped_measured = 0; // calibrated brute-force cost ratio flat / grouped (AUTO picks grouped above 1.25)
     DevBuf<NodeF> nodes;
@@ -1382,15 +1383,28 @@ int prepare_jit(rt_scene* s)
         s->jit.status = s->jit.fn ? 1 : (s->jit.error.empty() ? 0 : -1);
         return s->jit.fn ? 1 : 0;
     }
-    s->jit.error.clear();
-    s->jit.variant = s->variant;
-    s->jit.gen = gen;
-    if (s->jit.fn) jit_release(s->device, s->jit.fn); // launches still queued keep it: eviction syncs the device
-    s->jit.fn = nullptr;
     PathParams lp{};
     fill_launch(s->dev, s->variant, lp);
     const auto& B = grouped ? s->grouped_h : s->flat_h;
-    const std::string header = jit_scene_header(lp.scene, s->camf, B.groups, B.rects, B.frames, B.tests, s->xf_h);
+    // The grouped order's build carries the camera (its group order is per camera anyway); the flat
+    // order's only the camera's kind and depth-of-field switch, so moving the camera among cameras
+    // of one kind (MainWindow.cs:262-269 restarts the render with another scene camera) reuses the
+    // build: the same header, no hiprtc build and no cache lookup.
+    const std::string header =
+        jit_scene_header(lp.scene, s->camf, grouped, B.groups, B.rects, B.frames, B.tests, s->xf_h);
+    if (s->jit.variant == s->variant && s->jit.fn && header == s->jit.header) {
+        s->jit.gen = gen;
+        s->jit.status = 1;
+        s->jit.compile_ms = 0;
+        s->jit.from_cache = true;
+        return 1;
+    }
+    s->jit.error.clear();
+    s->jit.variant = s->variant;
+    s->jit.gen = gen;
+    s->jit.header = header;
+    if (s->jit.fn) jit_release(s->device, s->jit.fn); // launches still queued keep it: eviction syncs the device
+    s->jit.fn = nullptr;
     if (const char* dump = getenv("RTCORE_JIT_DUMP")) { // inspection: the generated header of the last build
         if (FILE* f = fopen(dump, "w")) {
             fwrite(header.data(), 1, header.size(), f);
@@ -1538,6 +1552,10 @@ int build_bvhs(rt_scene* s)
     for (int i = 0; i < n; i++)
         if (H[i].kind != RT_PRIM_PLANE) ids.push_back(i);
     const int nb = (int)ids.size();
+    if (nb + kTestSpares >= kLeafGenericMaxSlots) { // leaf codes (rt_internal.h) address 2^27 slots
+        set_error("rt_scene_create: more than 2^27 - " + std::to_string(kTestSpares) + " BVH primitives");
+        return RT_ERR_ARG;
+    }
     int max_leaf = n > 256 ? 3 : 2; // C4 mesh: leaves of <= 2, 3, 4, 6, 8 -> 70.6, 70.5, 72.2, 76.1, 80.2 ms
     if (const char* e = getenv("RTCORE_MAX_LEAF")) max_leaf = std::max(1, std::min(8, atoi(e))); // tuning
     s->bvh.builder = builder_for(nb);
@@ -1714,8 +1732,16 @@ int rt_debug_trace_rays(rt_scene* s, const void* d_rays, uint32_t n, void* d_hit
         set_error("rt_debug_trace_rays: needs a wide BVH and a scene without planes");
         return RT_ERR_STATE;
     }
+    // the trace-only kernel starts every query from no hit: the vertex-normal re-hit start of a
+    // logged query (Sample.prev <= -2, query_start) is not restated there
+    if (s->dev.n_vn > 0) {
+        set_error("rt_debug_trace_rays: scenes with vertex-normal triangles are not supported");
+        return RT_ERR_STATE;
+    }
     HIP_TRY(hipSetDevice(s->device));
     hipStream_t st = static_cast<hipStream_t>(stream);
+    // the work counter and the stack overflow area are the scene's: order after its last render
+    if (s->any_op && st != s->last_stream) HIP_TRY(hipStreamWaitEvent(st, s->done_ev, 0));
     const int grid = s->n_cu * trace_rays_blocks_per_cu(waves);
     HIP_TRY(s->stack_ovf.reserve((size_t)grid * 256 * kStackOverflow));
     HIP_TRY(s->counter.reserve(1));
@@ -1734,16 +1760,23 @@ int rt_debug_trace_rays(rt_scene* s, const void* d_rays, uint32_t n, void* d_hit
     p.spec = 16;
     if (const char* e = getenv("RTCORE_BVH_SPEC")) p.spec = std::max(1, std::min(64, atoi(e)));
     p.stats = static_cast<unsigned long long*>(d_stats);
-    hipEvent_t e0, e1;
-    HIP_TRY(hipEventCreate(&e0));
-    HIP_TRY(hipEventCreate(&e1));
-    HIP_TRY(hipEventRecord(e0, st));
+    struct Events { // destroyed on every exit path
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        ~Events()
+        {
+            if (e0) (void)hipEventDestroy(e0);
+            if (e1) (void)hipEventDestroy(e1);
+        }
+    } ev;
+    HIP_TRY(hipEventCreate(&ev.e0));
+    HIP_TRY(hipEventCreate(&ev.e1));
+    HIP_TRY(hipEventRecord(ev.e0, st));
     HIP_TRY(launch_trace_rays(p, waves, grid, st));
-    HIP_TRY(hipEventRecord(e1, st));
-    HIP_TRY(hipEventSynchronize(e1));
-    HIP_TRY(hipEventElapsedTime(ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
+    HIP_TRY(hipEventRecord(ev.e1, st));
+    const int rc = end_op(s, st);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(hipEventSynchronize(ev.e1));
+    HIP_TRY(hipEventElapsedTime(ms, ev.e0, ev.e1));
     return RT_OK;
 }
 
@@ -1858,6 +1891,10 @@ int rt_scene_check_bvh(rt_scene* s)
         const uint32_t lfl = leaf_flags(((uint32_t)(~ref) >> 25) & 31u);
         if (first < 0 || first + cnt > nb) {
             err = "leaf range out of bounds";
+            return;
+        }
+        if (compact && first + cnt > kLeafCompactMaxFirst) {
+            err = "compact leaf beyond the slots its code can address";
             return;
         }
         for (int k = first; k < first + cnt; k++) {

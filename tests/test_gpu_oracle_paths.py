@@ -225,6 +225,32 @@ def test_loader_commands_against_oracle(rc, name, mode):
     gpu.close()
 
 
+# The vertex-normal quads inside an inverted one-sided room (a closed cube, tested as one box record
+# by the brute-force orders) instead of over a plane: a diffuse bounce off a quad's back side leaves
+# along GetNormal's NaN normal from inside the room.  The reference's next query fails its BVH root
+# test (BVH.cs:301-303) and misses (ambient colour); the box record's slab reciprocals stay finite for
+# NaN, so the brute-force kernels must end such a query themselves.
+VN_ROOM_SCENE = VN_SCENE.replace("plane -1 0 0 1\n", "twosided false\ninvert true\ndiffuse .5 .5 .5\n"
+                                 "cube 0 0 2 6 6 7 all\n")
+
+
+@pytest.mark.parametrize("mode", ["BRUTE", "GROUPED", "BVH"])
+def test_vertexnormal_room_against_oracle(rc, mode):
+    """Vertex-normal back sides in a closed room, every traversal against the oracle."""
+    assert "cube 0 0 2 6 6 7 all" in VN_ROOM_SCENE
+    scene = rc.SceneLoader.from_text(VN_ROOM_SCENE)
+    size = (64, 48)
+    gpu = rc.GpuRaytracer(scene, 0, size=size, traversal=getattr(rc, "RT_TRAVERSAL_" + mode))
+    if mode != "BVH":
+        assert gpu.build_stats()["flat_boxes"] >= 1  # the room is one box record
+    orc = _oracle(rc, scene, size)
+    assert np.array_equal(gpu.primary_ids(), orc.primary_ids())
+    spp = 64
+    _assert_parity(gpu.render_tile(0, 0, *size, spp, seed=8), orc.render_tile(0, 0, *size, spp, seed=8), spp,
+                   label=f"vertexnormal room {mode}")
+    gpu.close()
+
+
 def test_vertexnormal_back_side_samples(rc):
     """Samples whose path meets a vertex-normal triangle from behind (NaN normal) agree with the
     oracle one by one (1-spp passes; misses are Placeholder)."""

@@ -14,10 +14,14 @@ and clipping it at 1 would bias the comparison downwards (die.png read 0.96-0.99
 48 spp); the linear means are unbiased, so only sampling noise remains: about 1 % at 192 spp
 over a few thousand pixels (seeds 1-3: die.png 0.990-1.002, app.png 0.991-1.010).
 
-* die.png (1280x960): captured at the file's exposure; radiance within 2.5 %.
+* die.png (1280x960): captured at the file's exposure; radiance within 2 %.
 * app.png: bounce.txt in the application window at the UI's exposure 1.000 (MainWindow.cs:40)
   after 4,826 spp, camera 0, recursion 10; its 700x700 viewport pins bounce.txt's radiance
-  within 3 % (FullRaytracer.cs:179-205).
+  within 2 % (FullRaytracer.cs:179-205).
+* Region by region (both screenshots): pixels grouped by the oracle's primary-ID map (the
+  DebugRaycaster Primitives mode, DebugRaycaster.cs:193-199), so that paths which cover few pixels
+  -- the Fresnel / TIR lens (primitive 20, Raytracer.cs:115-161), the spheres, the cut-out faces,
+  the die's faces and pips -- are each pinned on their own instead of inside one frame mean.
 * bounce-with-lens.png (1200x1200) was captured at an unknown exposure/recursion setting (its
   linear radiance is ~1.4x the file's recursion-10 render): geometry plus one uniform factor.
 """
@@ -63,17 +67,102 @@ def _linear_ratio(ref_rgb, lin, ok):
     return lin[ok].mean(axis=0) / (((ref_rgb[ok] + 0.5) / 255.0) ** 2.2).mean(axis=0)
 
 
+def _render_points(scene_file, size, pts, spp, seed):
+    """The oracle's linear per-pixel means [n, 3] and miss counts [n] at the pixels pts [(x, y)]."""
+    orc = OracleScene.from_file(os.path.join(GOLDEN, "scenes", scene_file))
+    orc.set_size(*size)
+    lin = np.zeros((len(pts), 3))
+    miss = np.zeros(len(pts), np.int64)
+    chunks = np.array_split(np.arange(len(pts)), 64)
+
+    def run(idx):  # ctypes releases the GIL: chunks render on the host cores in parallel
+        for k in idx:
+            s, n, m, _ = orc.render_tile(int(pts[k][0]), int(pts[k][1]), 1, 1, spp, seed=seed)
+            lin[k] = s[0, 0] / max(1, int(n[0, 0]))
+            miss[k] = m[0, 0]
+
+    with ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
+        list(ex.map(run, chunks))
+    return lin, miss
+
+
+def _region_ids(scene_file, size, xs, ys):
+    """The oracle's primary-ID map (exact; integer pixel, no jitter or depth of field) at the sparse
+    pixels, and whether each one's 3x3 neighbourhood holds one ID (away from region edges)."""
+    orc = OracleScene.from_file(os.path.join(GOLDEN, "scenes", scene_file))
+    orc.set_size(*size)
+    ids = orc.primary_ids()  # [x, y]
+    w, h = size
+    rid = ids[np.ix_(xs, ys)].T  # [y, x]
+    inner = np.ones_like(rid, bool)
+    for dx in (-1, 0, 1):
+        for dy in (-1, 0, 1):
+            inner &= ids[np.ix_(np.clip(xs + dx, 0, w - 1), np.clip(ys + dy, 0, h - 1))].T == rid
+    return rid, inner
+
+
+LUMA = np.array([0.299, 0.587, 0.114])  # DoubleColor.GetLuminance (DoubleColor.cs:76-79)
+
+
+def _check_regions(label, ref, lin, ok, rid, regions, tol, min_pixels=200, tol_of=None):
+    """Region by region: the oracle's mean linear radiance against the screenshot's, where a pixel's
+    code v only says its value lies in [v, v + 1) / 255 before the 2.2 power (truncation,
+    SampleSet.cs:61-113).  The deviation is the distance of the oracle's mean from the region's
+    interval [mean ((v / 255)^2.2), mean (((v + 1) / 255)^2.2)], relative; it is asserted within
+    `tol` for the region's luminance (0.299 R + 0.587 G + 0.114 B) and for every channel whose
+    mean code is at least 48.  A darker channel is only reported: one 8-bit step there is 4.5 % and
+    more of the linear value, and in die.png such channels are the light blurred in by the depth of
+    field from neighbouring regions (the -x face has no red albedo, die.txt:44-46, yet its pixels
+    carry red codes near its edges).  Returns {region: (pixels, deviation R, G, B, luminance)}."""
+    lo = (ref / 255.0) ** 2.2
+    hi = ((ref + 1.0) / 255.0) ** 2.2
+    out = {}
+    t_of = tol_of or {}
+    for name, m in regions:
+        m = m & ok & (ref.max(axis=-1) >= 16)  # near-black pixels say nothing of the radiance
+        n = int(m.sum())
+        if n < min_pixels:
+            continue
+        o, a, b = lin[m].mean(0), lo[m].mean(0), hi[m].mean(0)
+        o, a, b = np.append(o, o @ LUMA), np.append(a, a @ LUMA), np.append(b, b @ LUMA)
+        dev = np.where(o > b, o / b - 1, np.where(o < a, o / a - 1, 0.0))
+        code = np.append(ref[m].mean(0), 255.0)
+        t = t_of.get(name, tol)
+        checked = code >= 48
+        out[name] = (n, dev)
+        print(f"{label} region {name}: {n} px, mean code {np.round(code[:3], 1)}, deviation R G B Y "
+              f"{np.round(100 * dev, 2)} % (bound {100 * t:.0f} % on {''.join(c for c, k in zip('RGBY', checked) if k)})")
+        bad = checked & ~(np.abs(dev) <= t)
+        assert not bad.any(), f"{label} region {name}: deviation {dev} beyond {t}"
+    return out
+
+
 def test_die_screenshot_geometry_and_radiance():
+    """die.png: coverage (32 spp over every sampled pixel) and mean linear radiance of the fully
+    covered, unsaturated pixels within 2 % of the oracle (768 spp); then region by region: each die
+    face and each pip with at least 200 usable pixels, and the 21 pips together, within 4 %."""
     ref, xs, ys, size = _load("die")
-    assert size == (1280, 960)
-    got, lin, miss = _render_sparse("die.txt", size, xs, ys, 192)
+    assert size == (1280, 960) and ref.shape[:2] == (240, 320)
+    got, _, _ = _render_sparse("die.txt", size, xs, ys, 32)
     agree = ((ref[..., 3] > 0) == (got[..., 3] > 0)).mean()
     assert agree > 0.985, f"coverage agreement {agree:.4f}"
-    ok = (ref[..., 3] == 255) & (miss == 0) & np.all(ref[..., :3] < 250, axis=-1)
-    assert ok.sum() > 1000
+    cand = (ref[..., 3] == 255) & np.all(ref[..., :3] < 250, axis=-1)
+    jj, ii = np.nonzero(cand)
+    pts = list(zip(xs[ii], ys[jj]))
+    lin_p, miss_p = _render_points("die.txt", size, pts, 768, seed=1)
+    lin = np.zeros(ref.shape[:2] + (3,))
+    miss = np.ones(ref.shape[:2], np.int64)
+    lin[jj, ii], miss[jj, ii] = lin_p, miss_p
+    ok = cand & (miss == 0)
+    assert ok.sum() > 8000
     ratio = _linear_ratio(ref[..., :3], lin, ok)
     print("die.png radiance ratio (R, G, B):", ratio, "pixels", int(ok.sum()))
-    assert np.all(np.abs(ratio - 1) < 0.025), ratio
+    assert np.all(np.abs(ratio - 1) < 0.02), ratio
+    # regions: die faces 2-7 (-y, +y, +x, -x, -z, +z) and pips 8-28 (die.txt:32-87, SURVEY 8(a))
+    rid, inner = _region_ids("die.txt", size, xs, ys)
+    regions = [(int(r), rid == r) for r in range(2, 29)] + [("pips", (rid >= 8) & (rid <= 28))]
+    out = _check_regions("die.png", ref[..., :3], lin, ok & inner, rid, regions, 0.04)
+    assert {7, "pips"} <= set(out) and len(out) >= 6, sorted(map(str, out))
 
 
 def test_bounce_screenshot_geometry_and_uniform_exposure():
@@ -99,18 +188,35 @@ def test_bounce_screenshot_geometry_and_uniform_exposure():
     assert ratios.std() / ratios.mean() < 0.15, ratios
 
 
+# Sphere 13 (bounce.txt:88, diffuse .9 / specular .2 at shininess 250) is the one region of app.png
+# near the 4 % bound: past the quantisation interval it reads -3.6 / -1.3 / -2.4 % (R, G, B) here
+# (1,024 oracle spp, seed 1), -3.9 / -1.8 / -2.8 % at 3,072 spp (seed 2), and its mid-interval R
+# ratio spans 0.93-0.955 over five seeds at 768 spp.  The oracle-side noise (about 1 % between
+# seeds) does not account for it; the screenshot's own noise at 4,826 spp on a glossy surface may.
+# It is held at 7 % and reported, every other region at 4 %.
+APP_REGION_TOL = {13: 0.07}
+
+
 def test_bounce_app_screenshot_exposure1_radiance():
-    """bounce.txt at exposure 1.000 (Screenshots/app.png viewport): coverage, and per-channel mean
-    linear radiance of the fully covered, unsaturated pixels within 3 % of the oracle."""
+    """bounce.txt at exposure 1.000 (Screenshots/app.png viewport, every 4th pixel): coverage, the
+    per-channel mean linear radiance of the fully covered, unsaturated pixels within 2 % of the
+    oracle (1,024 spp), and region by region: every primitive with at least 200 usable pixels --
+    the room's walls, floor and ceiling, the cut-out faces, sphere 13, the rotated cube's faces and
+    the Fresnel / TIR lens (20) -- within 4 % (sphere 13: APP_REGION_TOL)."""
     d = np.load(os.path.join(GOLDEN, "screenshot_app_bounce700.npz"))
     ref, xs, ys = d["rgb"].astype(np.int64), d["xs"], d["ys"]
-    assert tuple(d["size"]) == (700, 700) and float(d["exposure"][0]) == 1.0
-    got, lin, miss = _render_sparse("bounce.txt", (700, 700), xs, ys, 192)
+    assert tuple(d["size"]) == (700, 700) and float(d["exposure"][0]) == 1.0 and ref.shape[:2] == (175, 175)
+    got, lin, miss = _render_sparse("bounce.txt", (700, 700), xs, ys, 1024)
     panel = np.all(ref == d["panel"], axis=-1)  # a transparent (all-miss) pixel shows the panel grey
     agree = (panel != (got[..., 3] > 0)).mean()
-    assert agree > 0.99, f"coverage agreement {agree:.4f}"
+    assert agree > 0.985, f"coverage agreement {agree:.4f}"
     ok = (miss == 0) & ~panel & np.all(ref < 250, axis=-1)
-    assert ok.sum() > 2000
+    assert ok.sum() > 10000
     ratio = _linear_ratio(ref, lin, ok)
     print("app.png exposure-1 radiance ratio (R, G, B):", ratio, "pixels", int(ok.sum()))
-    assert np.all(np.abs(ratio - 1) < 0.03), ratio
+    assert np.all(np.abs(ratio - 1) < 0.02), ratio
+    rid, inner = _region_ids("bounce.txt", (700, 700), xs, ys)
+    regions = [(int(r), rid == r) for r in range(22)]
+    out = _check_regions("app.png", ref, lin, ok & inner, rid, regions, 0.04, tol_of=APP_REGION_TOL)
+    # the lens, sphere 13, the floor (10), the far walls (6, 9) and a rotated-cube face must be among them
+    assert {6, 9, 10, 13, 20} <= set(out) and len(out) >= 8, sorted(out)

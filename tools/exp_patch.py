@@ -1,0 +1,97 @@
+"""Cost experiments on the path kernels, kept out of the product source.
+
+Copies raytracercore_amd/csrc (and include/) into raytracercore_amd/variants/NAME/tree, applies the
+named textual patches below to the copy of kernels_path.hip, and builds the library there
+(raytracercore_amd/variants/NAME/librtcore_hip.so; load it with RTCORE_LIB=<path>).  The copy's
+sources are what its scene-specialised builds embed, so the patches reach them too.
+
+usage: python tools/exp_patch.py NAME PATCH[,PATCH...] ["EXTRA hipcc flags"]
+       python tools/exp_patch.py --list
+A patch is a list of (anchor, replacement) pairs; every anchor must occur exactly once.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "raytracercore_amd", "csrc")
+
+TRACE_CALL = ("            trace_brute<CULL, STATS>(sc, groups, tests, rects, frames, boxes, xf, S.o, S.d, S.prev, b, cnt.tris,\n"
+              "                                     cnt.sphs, cnt.nodes);\n")
+BOUNCE_CALL = "            bounce<VN>(L, S, sc, R, vnormals, tests, pq->prims_d, b);\n"
+RAYS_LINE = "        wave_rays += (unsigned)__popcll(__ballot(L.live)); // one Scene.RayTrace per live lane\n"
+
+PATCHES = {
+    # every camera ray misses: the per-sample overhead alone
+    "NO_TRACE": [(TRACE_CALL, "")],
+    # a second bounce on a copy of the sample: the shading section's cost
+    "DUP_SHADE": [(BOUNCE_CALL,
+                   "            {\n"
+                   "                Sample S2 = S;\n"
+                   "                S2.rng.k0 ^= (unsigned)S.bounce;\n"
+                   "                V3 c2;\n"
+                   "                shade<VN>(sc, R.prims, R.mats, R.xfs, vnormals, tests, pq->prims_d, b, S2, c2);\n"
+                   "                if (c2.x + S2.d.x == 1234.5f) pq->partial[0].x = 1.0f;\n"
+                   "            }\n" + BOUNCE_CALL)],
+    # a second camera sample on a copy: the sample start's cost
+    "DUP_START": [(RAYS_LINE,
+                   "        if (L.live) {\n"
+                   "            Sample S2 = S;\n"
+                   "            S2.rng.k0 ^= (unsigned)S.bounce;\n"
+                   "            start_sample<true>(*cp, L.fx, L.fy, S2);\n"
+                   "            if (S2.o.x + S2.d.y == 1234.5f) pq->partial[0].x = 1.0f;\n"
+                   "        }\n" + RAYS_LINE)],
+    # no depth of field in the sample start
+    "NO_DOF": [("    if (cam_dof(cam)) {\n", "    if (false) {\n")],
+    # the bounce direction never renormalised (round 3's brute-force form)
+    "NO_RENORM": [("    S.d = out_dir * (renormalise_at<SLOT>(s, S.bounce + 1) ? fmaf(-0.5f, dot(out_dir, out_dir), 1.5f) : 1.0f);\n",
+                   "    S.d = SLOT ? normalize(out_dir) : out_dir;\n")],
+    # the renormalisation test as a plain remainder in every kernel
+    "RENORM_MOD3": [("    if (SLOT) return (unsigned)i % 3u == 0u;\n", "    return (unsigned)i % 3u == 0u;\n")],
+    # no literal folding of zero scene fields in the specialised build
+    "NO_KFOLD": [("    return __builtin_constant_p(c) && c == 0.0f;\n", "    return false;\n")],
+}
+
+
+def apply(src: str, names: list[str]) -> str:
+    for name in names:
+        for anchor, repl in PATCHES[name]:
+            n = src.count(anchor)
+            if n != 1:
+                sys.exit(f"patch {name}: anchor found {n} times:\n{anchor}")
+            src = src.replace(anchor, repl)
+    return src
+
+
+def main() -> None:
+    if len(sys.argv) >= 2 and sys.argv[1] == "--list":
+        print("\n".join(sorted(PATCHES)))
+        return
+    if len(sys.argv) < 3:
+        sys.exit(__doc__)
+    name, names = sys.argv[1], [p for p in sys.argv[2].split(",") if p and p != "NONE"]
+    extra = sys.argv[3] if len(sys.argv) > 3 else ""
+    for p in names:
+        if p not in PATCHES:
+            sys.exit(f"unknown patch {p} (known: {', '.join(sorted(PATCHES))})")
+    out = os.path.join(ROOT, "raytracercore_amd", "variants", name)
+    tree = os.path.join(out, "tree")
+    shutil.rmtree(tree, ignore_errors=True)
+    shutil.copytree(os.path.join(ROOT, "include"), os.path.join(tree, "include"))
+    dst = os.path.join(tree, "pkg", "csrc")
+    shutil.copytree(CSRC, dst, ignore=shutil.ignore_patterns("_obj*"))
+    kp = os.path.join(dst, "kernels_path.hip")
+    with open(kp) as f:
+        src = f.read()
+    with open(kp, "w") as f:
+        f.write(apply(src, names))
+    jobs = str(min(16, os.cpu_count() or 8))
+    subprocess.run(["make", "-s", "-C", dst, "-j" + jobs, "OUT=" + out, "EXTRA=" + extra], check=True)
+    print(os.path.join(out, "librtcore_hip.so"))
+
+
+if __name__ == "__main__":
+    main()
