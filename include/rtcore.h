@@ -207,6 +207,13 @@ int rt_scene_get_jit_error(const rt_scene* scene, char* buf, int32_t cap);
    as a scene-specialised build of an empty scene; returns the code object size, or a negative
    rt_status with the compiler log in `log` (may be NULL). */
 int rt_debug_jit_compile(const char* arch, int32_t grouped, char* log, int32_t cap);
+/* Host only (no device needed): the generated header of the scene-specialised build that
+   rt_scene_create + rt_scene_set_camera would make for these primitives and camera (grouped = 0
+   flat order, 1 grouped order; brute-force scenes of <= 48 primitives), for reading its code
+   without a GPU (tools/jit_isa.py).  Returns the header length; copies it NUL-terminated into buf
+   when cap exceeds the length. */
+int rt_debug_jit_header(const rt_scene_params* params, const rt_prim* prims, int32_t n_prims, const rt_camera* camera,
+                        int32_t grouped, char* buf, int64_t cap);
 /* Validation: checks the device-resident BVH2 and wide tree against the primitives (every
    child box contains the primitives below it, each primitive in exactly one leaf, depth and
    stack within what the kernels were sized for).  RT_ERR_STATE with the finding otherwise. */

@@ -134,6 +134,8 @@ def load_library(path: str = "") -> C.CDLL:
         "rt_set_jit": (C.c_int, [C.c_int32]),
         "rt_scene_get_jit_error": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32]),
         "rt_debug_jit_compile": (C.c_int, [C.c_char_p, C.c_int32, C.c_char_p, C.c_int32]),
+        "rt_debug_jit_header": (C.c_int, [P(rt_scene_params), P(rt_prim), C.c_int32, P(rt_camera), C.c_int32,
+                                          C.c_char_p, C.c_int64]),
         "rt_render_tile": (C.c_int, [C.c_void_p] + [C.c_int32] * 5 + [C.c_uint64, C.c_uint64,
                                      P(rt_color), P(C.c_uint32), P(C.c_uint32), P(C.c_uint64)]),
         "rt_render_tile_1spp": (C.c_int, [C.c_void_p] + [C.c_int32] * 4 + [C.c_uint64, C.c_uint64, P(rt_color)]),
@@ -224,6 +226,27 @@ class SceneLoader:
 
 LAYOUT_NAMES = ("rects", "boxes", "frames", "frame_boxes", "frame_rects", "tris", "spheres", "planes",
                 "groups", "grouped_slots")
+
+
+def jit_header(scene: "SceneLoader", camera: int = 0, size: Optional[Tuple[int, int]] = None,
+               grouped: bool = False) -> str:
+    """rt_debug_jit_header (host code, no GPU): the generated header of the scene-specialised build
+    for this scene and camera (tools/jit_isa.py compiles it and writes the listing)."""
+    lib = load_library()
+    params = rt_scene_params.from_buffer_copy(scene.params)
+    if size:
+        params.width, params.height = size
+    n = len(scene.prims)
+    arr = (rt_prim * max(1, n))(*scene.prims)
+    cam = rt_camera.from_buffer_copy(scene.cameras[camera])
+    k = lib.rt_debug_jit_header(C.byref(params), arr, n, C.byref(cam), 1 if grouped else 0, None, 0)
+    if k < 0:
+        _check(k)
+    buf = C.create_string_buffer(k + 1)
+    k2 = lib.rt_debug_jit_header(C.byref(params), arr, n, C.byref(cam), 1 if grouped else 0, buf, k + 1)
+    if k2 < 0:
+        _check(k2)
+    return buf.value.decode()
 
 
 def brute_layout(prims: Sequence[rt_prim]) -> dict:
@@ -378,9 +401,14 @@ class GpuRaytracer:
                                                C.c_void_p(d_sum), C.c_void_p(d_samples), C.c_void_p(d_misses), plane,
                                                C.c_void_p(d_rays), C.c_void_p(stream)))
 
-    def render_tile_1spp(self, x0: int, y0: int, w: int, h: int, seed: int = 0, sample_index: int = 0) -> np.ndarray:
-        """Raytracer.Render one pass: DoubleColor[w, h] with Placeholder (-1) for misses."""
-        out = np.empty((w, h, 3), np.float64)
+    def render_tile_1spp(self, x0: int, y0: int, w: int, h: int, seed: int = 0, sample_index: int = 0,
+                         out: Optional[np.ndarray] = None) -> np.ndarray:
+        """Raytracer.Render one pass: DoubleColor[w, h] with Placeholder (-1) for misses (into `out`,
+        a C-contiguous float64 [w, h, 3] array, when given)."""
+        if out is None:
+            out = np.empty((w, h, 3), np.float64)
+        elif out.shape != (w, h, 3) or out.dtype != np.float64 or not out.flags.c_contiguous:
+            raise ValueError("out must be a C-contiguous float64 array of shape (w, h, 3)")
         _check(self.lib.rt_render_tile_1spp(self.handle, x0, y0, w, h, seed, sample_index,
                                             out.ctypes.data_as(C.POINTER(rt_color))))
         return out

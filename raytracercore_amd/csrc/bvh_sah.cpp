@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "host_scene.h"
@@ -285,11 +286,10 @@ struct W4Builder {
     std::vector<Node4Q> out;
     int stack_need = 0;
     int depth = 0;
+    bool siblings = false; // sibling-adjacent order: a node's internal children get consecutive indices
 
-    // Emit the wide node for BVH2 node i (pre-order); returns its index.
-    int emit(int i, int level, int pushes)
+    std::vector<WChild> children(int i) const
     {
-        depth = std::max(depth, level);
         std::vector<WChild> ch{{nodef_box(n2[i], false), nodef_ref(n2[i], false)},
                                {nodef_box(n2[i], true), nodef_ref(n2[i], true)}};
         while (ch.size() < 4) {
@@ -306,13 +306,59 @@ struct W4Builder {
             ch[best] = a;
             ch.insert(ch.begin() + best + 1, b);
         }
+        return ch;
+    }
+
+    // Emit the wide node for BVH2 node i at index `me` (already allocated); pre-order, or with its
+    // internal children allocated as one consecutive block before any of their subtrees.
+    void emit_at(int me, int i, int level, int pushes)
+    {
+        depth = std::max(depth, level);
+        const std::vector<WChild> ch = children(i);
+        const int nc = (int)ch.size();
+        stack_need = std::max(stack_need, pushes + nc - 1);
+        int refs[4] = {RT_NODE4_EMPTY, RT_NODE4_EMPTY, RT_NODE4_EMPTY, RT_NODE4_EMPTY};
+        if (siblings) {
+            for (int k = 0; k < nc; k++)
+                if (ch[k].ref >= 0) {
+                    refs[k] = (int)out.size();
+                    out.push_back(Node4Q{});
+                }
+            for (int k = 0; k < nc; k++) {
+                if (ch[k].ref >= 0) emit_at(refs[k], ch[k].ref, level + 1, pushes + nc - 1);
+                else refs[k] = ch[k].ref;
+            }
+        } else {
+            for (int k = 0; k < nc; k++)
+                refs[k] = ch[k].ref >= 0 ? emit(ch[k].ref, level + 1, pushes + nc - 1) : ch[k].ref;
+        }
+        float lo[4][3], hi[4][3];
+        for (int k = 0; k < nc; k++)
+            for (int a = 0; a < 3; a++) {
+                lo[k][a] = ch[k].box.lo[a];
+                hi[k][a] = ch[k].box.hi[a];
+            }
+        out[me] = quantize_node4(lo, hi, refs, nc);
+    }
+    int emit(int i, int level, int pushes)
+    {
+        const int me = (int)out.size();
+        out.push_back(Node4Q{});
+        emit_at(me, i, level, pushes);
+        return me;
+    }
+    // Emit the wide node for BVH2 node i (pre-order); returns its index.
+    int emit_pre(int i, int level, int pushes)
+    {
+        depth = std::max(depth, level);
+        const std::vector<WChild> ch = children(i);
         const int me = (int)out.size();
         out.push_back(Node4Q{});
         const int nc = (int)ch.size();
         stack_need = std::max(stack_need, pushes + nc - 1);
         int refs[4] = {RT_NODE4_EMPTY, RT_NODE4_EMPTY, RT_NODE4_EMPTY, RT_NODE4_EMPTY};
         for (int k = 0; k < nc; k++)
-            refs[k] = ch[k].ref >= 0 ? emit(ch[k].ref, level + 1, pushes + nc - 1) : ch[k].ref;
+            refs[k] = ch[k].ref >= 0 ? emit_pre(ch[k].ref, level + 1, pushes + nc - 1) : ch[k].ref;
         float lo[4][3], hi[4][3];
         for (int k = 0; k < nc; k++)
             for (int a = 0; a < 3; a++) {
@@ -453,8 +499,9 @@ Bvh4 build_bvh4(const SahBvh& b2, const WideCosts* sah)
         return r;
     }
     W4Builder w{b2.nodes, {}, 0, 0};
+    if (const char* e = getenv("RTCORE_WIDE_ORDER")) w.siblings = e[0] == 's'; // A/B: sibling-adjacent order
     w.out.reserve(b2.nodes.size() / 2 + 1);
-    r.root = w.emit(0, 0, 0);
+    r.root = w.siblings ? w.emit(0, 0, 0) : w.emit_pre(0, 0, 0);
     r.nodes = std::move(w.out);
     r.stack_need = w.stack_need;
     r.depth = w.depth;

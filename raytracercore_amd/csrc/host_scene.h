@@ -1,6 +1,7 @@
 // host_scene.h -- host-side preparation of a scene for the MI355X kernels.
 #pragma once
 #include <algorithm>
+#include <functional>
 #include <string>
 #include <thread>
 #include <vector>
@@ -9,43 +10,40 @@
 
 namespace rtc {
 
-// fn(i) for i in [0, n) on up to 16 host threads (at least 4096 items each); fn must only
-// write state of its own index.
+// Runs task(i) for every i in [0, n) on the process's persistent host worker pool (host_pool.cpp:
+// up to 16 threads, OMP_NUM_THREADS where set, the caller included) and returns when all are done.
+void host_run(size_t n, const std::function<void(size_t)>& task);
+int host_threads();
+
+// fn(i) for i in [0, n) on the host pool (at least 4096 items per thread); fn must only write state
+// of its own index.
 template <class F>
 void parallel_for(int n, F&& fn)
 {
-    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
-    const int T = std::min(std::min(hw, 16), (n + 4095) / 4096);
+    const int T = std::min(host_threads(), (n + 4095) / 4096);
     if (T <= 1) {
         for (int i = 0; i < n; i++) fn(i);
         return;
     }
-    std::vector<std::thread> th;
     const int per = (n + T - 1) / T;
-    for (int t = 0; t < T; t++)
-        th.emplace_back([&fn, t, per, n] {
-            const int a = t * per, b = std::min(n, a + per);
-            for (int i = a; i < b; i++) fn(i);
-        });
-    for (auto& x : th) x.join();
+    host_run((size_t)T, [&](size_t t) {
+        const int a = (int)t * per, b = std::min(n, a + per);
+        for (int i = a; i < b; i++) fn(i);
+    });
 }
 
-// fn(a, b) over contiguous ranges covering [0, n) on up to 16 host threads, each range at least
-// min_items long (streaming passes over large arrays).
+// fn(a, b) over contiguous ranges covering [0, n) on the host pool, each range at least min_items
+// long (streaming passes over large arrays).
 template <class F>
 void parallel_ranges(size_t n, size_t min_items, F&& fn)
 {
-    const size_t hw = std::max(1u, std::thread::hardware_concurrency());
-    const size_t T = std::max<size_t>(1, std::min(std::min<size_t>(hw, 16), n / std::max<size_t>(1, min_items)));
+    const size_t T = std::max<size_t>(1, std::min<size_t>((size_t)host_threads(), n / std::max<size_t>(1, min_items)));
     if (T <= 1) {
         fn((size_t)0, n);
         return;
     }
-    std::vector<std::thread> th;
     const size_t per = (n + T - 1) / T;
-    for (size_t t = 0; t < T; t++)
-        th.emplace_back([&fn, t, per, n] { fn(std::min(n, t * per), std::min(n, (t + 1) * per)); });
-    for (auto& x : th) x.join();
+    host_run(T, [&](size_t t) { fn(std::min(n, t * per), std::min(n, (t + 1) * per)); });
 }
 
 // Axis-aligned box in the reference's fp64 representation (Acceleration/AABB.cs:44-64).

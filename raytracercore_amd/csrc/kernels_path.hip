@@ -24,6 +24,15 @@
 // primitive branch-free.  BVH traversal keeps a per-lane stack in LDS.
 #include "../../include/rtcore_rng.h"
 #include "rt_kernels.h"
+#ifdef RT_SCENE_CONST
+// rt_jit.cpp generates this header per scene (and camera, for the grouped order): the launch's
+// PathScene and its brute-force records as 32-bit words (kSceneW, kGroupsW, kRectsW, kFramesW,
+// kTestsW, kXfW, kCameraW) and the camera switches (RT_SCENE_CAMERA_KIND / _DOF).  Every record
+// field then folds into the instructions (literal operands cost what a VGPR operand does on
+// gfx950, an SGPR operand twice that), the primitive loops unroll and the per-record flag branches
+// resolve at compile time.  Included first, so that every macro it defines is seen by the code.
+#include "rt_scene_const.h"
+#endif
 
 namespace rtc {
 namespace {
@@ -76,8 +85,9 @@ __device__ __forceinline__ int pack_sg(int slot, bool gin) { return (slot << 1) 
 
 // Triangle via the affine inverse record (TestRec): w(t) = 0 gives t, then (u, v).
 // Inside (Moller-Trumbore's 1/det < 0, Triangle.cs:127) <=> d . n > 0 <=> dw > 0.
-// The BVH kernels name the primitive a ray leaves by its slot (SLOT: id = slot, Sample.prev = slot),
-// so that the records of compact leaves carry no ID; the brute-force kernels by its primitive ID.
+// Every kernel names the primitive a ray leaves by its slot (SLOT: id = slot, Sample.prev = slot): a
+// hit-able primitive has exactly one slot in each order, the records of compact leaves carry no ID,
+// and a box names its faces' slots by face index (sg0 / 2 + f) without a table.
 __device__ __forceinline__ void hit_tri_rows(float4 r0, float4 r1, float4 r2, uint32_t fl, int id, int slot, V3 o, V3 d,
                                              int prev, Best& b)
 {
@@ -176,7 +186,7 @@ __device__ __forceinline__ void hit_rect(const RectRec& R, int sg, V3 o, V3 d, V
     const bool in2 = fabsf(fmaf(t, d2, o2) - R.m2) <= R.h2;
     // 0 <= t < best as one unsigned compare of the bit patterns (b.t >= 0; NaN and -t fail)
     const bool near = __float_as_uint(t) < __float_as_uint(b.t);
-    const bool ok = near & in1 & in2 & (kmul(R.cull, da) <= 0.0f) & (R.id != prev);
+    const bool ok = near & in1 & in2 & (kmul(R.cull, da) <= 0.0f) & ((R.sg >> 1) != prev); // prev: a slot
     b.t = ok ? t : b.t; // the shading step rebuilds the hit point from t
     b.sg = ok ? sg : b.sg;
 }
@@ -258,20 +268,20 @@ __device__ __forceinline__ void hit_box(const BoxRec& B, V3 o, V3 d, V3 id, V3 o
     // the ray enters axis a's slab by its lower plane (side 0) when d[a] > 0
     const int sx = (int)(__float_as_uint(d.x) >> 31), sy = (int)(__float_as_uint(d.y) >> 31),
               sz = (int)(__float_as_uint(d.z) >> 31);
-    const uint32_t perm = __float_as_uint(B.hi.w), keep = B.keep;
-    const uint32_t rel_prev = (uint32_t)(prev - __float_as_int(B.lo.w)); // face IDs: id0 + (perm >> 4f & 15)
+    const uint32_t keep = B.keep;
+    const uint32_t rel_prev = (uint32_t)(prev - (B.sg0 >> 1)); // the face slot the ray leaves, relative to face 0
     bool ok_e = false, ok_x = false;
     int fe = 0, fo = 0;
     if (keep & 0x3Fu) { // some face keeps entry hits (wave-uniform)
         fe = te == nx ? sx : (te == ny ? 2 + sy : 4 + sz);
         // the keep bit is tested unconditionally: selecting on "every face keeps" cost more, and
         // folding that case in the scene-specialised build measured no change (round 3)
-        ok_e = meet & (__float_as_uint(te) < __float_as_uint(b.t)) & (((perm >> (4 * fe)) & 15u) != rel_prev) &
+        ok_e = meet & (__float_as_uint(te) < __float_as_uint(b.t)) & ((uint32_t)fe != rel_prev) &
                (((keep >> fe) & 1u) != 0);
     }
     if (keep & 0x3F00u) { // some face keeps exit hits
         fo = tx == fx ? 1 - sx : (tx == fy ? 3 - sy : 5 - sz);
-        ok_x = meet & (__float_as_uint(tx) < __float_as_uint(b.t)) & (((perm >> (4 * fo)) & 15u) != rel_prev) &
+        ok_x = meet & (__float_as_uint(tx) < __float_as_uint(b.t)) & ((uint32_t)fo != rel_prev) &
                (((keep >> (8 + fo)) & 1u) != 0);
     }
     const bool ok = ok_e | ok_x;
@@ -376,7 +386,7 @@ __device__ __forceinline__ void trace_brute(const SceneT& s, GroupP groups, Test
             TestRec cur = tests[i];
             for (; i < end; i++) {
                 const TestRec nxt = tests[i + 1];
-                hit_tri(cur, i, o, d, prev, b);
+                hit_tri<true>(cur, i, o, d, prev, b);
                 cur = nxt;
             }
         }
@@ -385,7 +395,7 @@ __device__ __forceinline__ void trace_brute(const SceneT& s, GroupP groups, Test
             TestRec cur = tests[i];
             for (; i < end; i++) {
                 const TestRec nxt = tests[i + 1];
-                hit_sph(cur, i, o, d, prev, xf, b);
+                hit_sph<true>(cur, i, o, d, prev, xf, b);
                 cur = nxt;
             }
         }
@@ -882,7 +892,7 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
     // rounding, so one Newton step of 1/|d| (1.5 - 0.5 |d|^2, relative error (|d|^2 - 1)^2) is the
     // normalisation to fp32 precision, without the reciprocal square root.
     S.d = out_dir * (renormalise_at<SLOT>(s, S.bounce + 1) ? fmaf(-0.5f, dot(out_dir, out_dir), 1.5f) : 1.0f);
-    S.prev = SLOT ? (b.sg >> 1) : id; // the BVH kernels name the left primitive by its slot
+    S.prev = b.sg >> 1; // the primitive the ray leaves, named by its slot (every kernel)
     if (VN && s.n_vn > 0 && kind == RT_PRIM_TRIANGLE && (fl & F_HASNORMALS)) {
         // does the reference's next query meet this triangle again (vn_rehit_test), and is that a
         // new hit?  Primitive.RayTrace culls it first when one-sided (Primitive.cs:56-64).  A NaN
@@ -1156,14 +1166,6 @@ __device__ __forceinline__ void flush_counts(unsigned long long wave_rays, const
 #else
 #define RT_AS_CONST // the host pass only needs the types
 #endif
-#ifdef RT_SCENE_CONST
-// rt_jit.cpp generates this header per scene (and camera, for the grouped order): the launch's
-// PathScene and its brute-force records as 32-bit words (kSceneW, kGroupsW, kRectsW, kFramesW,
-// kTestsW).  Every record field then folds into the instructions (literal operands cost what a
-// VGPR operand does on gfx950, an SGPR operand twice that), the primitive loops unroll and the
-// per-record flag branches resolve at compile time.
-#include "rt_scene_const.h"
-#endif
 typedef RT_AS_CONST const CameraF CameraC;
 typedef RT_AS_CONST const PathParams ParamsC;
 
@@ -1236,7 +1238,7 @@ __device__ __forceinline__ void path_body(const CameraF* __restrict__ camp, cons
             const int pln0 = sc.n_bvh;
             for (int i = pln0; i < pln0 + sc.n_pln; i++) {
                 const TestRec tr = tests[i];
-                hit_plane(tr, i, S.o, S.d, S.prev, b);
+                hit_plane<true>(tr, i, S.o, S.d, S.prev, b);
             }
             // A NaN direction (a diffuse bounce about GetNormal's NaN normal, only in scenes with
             // vertex-normal triangles) fails the reference's BVH root test (BVH.cs:301-303: far >= 0
@@ -1709,37 +1711,41 @@ __global__ void tonemap_kernel(int w, int h, const double* __restrict__ sum, con
     argb[i] = (int32_t)color_code(pow(r, gamma), pow(g, gamma), pow(b, gamma), a);
 }
 
-__global__ void colors_1spp_kernel(PathParams p, double* out)
+// One pass of Raytracer.Render (1 spp): DoubleColor[w, h] with Placeholder (-1) on a primary miss,
+// in the caller's order x * h + y, as fp32 -- a sample's colour is fp32 in the kernel, so the host
+// widens it to double exactly, and the PCIe copy is 12 B per pixel instead of 24.
+__global__ void colors_1spp_kernel(PathParams p, float* __restrict__ out)
 {
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
-    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= p.w || y >= p.h) return;
+    const size_t npix = (size_t)p.w * p.h;
+    const size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= npix) return;
+    const int x = (int)(o / (size_t)p.h), y = (int)(o - (size_t)x * p.h);
     const int q = ((y >> 3) * p.blocks_x + (x >> 3)) * 64 + (y & 7) * 8 + (x & 7); // 1 spp: one chunk
     const float4 v = p.partial[q];
     const bool miss = (__float_as_uint(v.w) & 0xFFFFu) == 0;
-    const size_t o = ((size_t)x * p.h + y) * 3; // DoubleColor[w, h]: x*h + y
-    out[o + 0] = miss ? -1.0 : (double)v.x;
-    out[o + 1] = miss ? -1.0 : (double)v.y;
-    out[o + 2] = miss ? -1.0 : (double)v.z;
+    out[3 * o + 0] = miss ? -1.0f : v.x;
+    out[3 * o + 1] = miss ? -1.0f : v.y;
+    out[3 * o + 2] = miss ? -1.0f : v.z;
 }
 
-// Planar row-major tile accumulators -> the caller's SampleSet order (C# [x, y]: x*h + y), so
-// that the host-buffer entry point copies one contiguous image and adds it sequentially:
-// rgb interleaved (DoubleColor), then samples, then misses.
+// Planar row-major tile accumulators -> the caller's SampleSet order (C# [x, y]: x * h + y), one
+// 32-B record per pixel (DoubleColor, samples, misses), so that the host-buffer entry point copies
+// one contiguous image in chunks and adds each chunk sequentially as it lands.
 __global__ void tile_host_layout_kernel(int w, int h, const double* __restrict__ sum, const uint32_t* __restrict__ ns,
-                                        const uint32_t* __restrict__ ms, double* __restrict__ rgb,
-                                        uint32_t* __restrict__ on, uint32_t* __restrict__ om)
+                                        const uint32_t* __restrict__ ms, TileRec* __restrict__ out)
 {
     const size_t npix = (size_t)w * h;
     const size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (o >= npix) return;
     const size_t x = o / (size_t)h, y = o - x * (size_t)h;
     const size_t i = y * (size_t)w + x;
-    rgb[3 * o + 0] = sum[i];
-    rgb[3 * o + 1] = sum[npix + i];
-    rgb[3 * o + 2] = sum[2 * npix + i];
-    on[o] = ns[i];
-    om[o] = ms[i];
+    TileRec r;
+    r.r = sum[i];
+    r.g = sum[npix + i];
+    r.b = sum[2 * npix + i];
+    r.samples = ns[i];
+    r.misses = ms[i];
+    out[o] = r;
 }
 
 // ---- compact leaves (rt_internal.h): 48-B rows and homogeneous leaf references --------------
@@ -1979,13 +1985,12 @@ hipError_t launch_tonemap(int w, int h, const double* d_sum, const uint32_t* d_s
 }
 
 hipError_t launch_tile_host_layout(int w, int h, const double* d_sum, const uint32_t* d_samples,
-                                  const uint32_t* d_misses, double* d_rgb, uint32_t* d_n, uint32_t* d_m,
-                                  hipStream_t stream)
+                                  const uint32_t* d_misses, TileRec* d_out, hipStream_t stream)
 {
     const size_t npix = (size_t)w * h;
     if (npix == 0) return hipSuccess;
     hipLaunchKernelGGL(tile_host_layout_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream, w, h, d_sum,
-                       d_samples, d_misses, d_rgb, d_n, d_m);
+                       d_samples, d_misses, d_out);
     return hipGetLastError();
 }
 
@@ -2040,10 +2045,11 @@ hipError_t launch_pixel_keys(rt_key2 seed_key, int w, int h, rt_key2* out, hipSt
     return hipGetLastError();
 }
 
-hipError_t launch_colors_1spp(const PathParams& p, double* d_out, hipStream_t stream)
+hipError_t launch_colors_1spp(const PathParams& p, float* d_out, hipStream_t stream)
 {
-    dim3 grid((p.w + 15) / 16, (p.h + 15) / 16);
-    hipLaunchKernelGGL(colors_1spp_kernel, grid, dim3(256), 0, stream, p, d_out);
+    const size_t npix = (size_t)p.w * p.h;
+    if (npix == 0) return hipSuccess;
+    hipLaunchKernelGGL(colors_1spp_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream, p, d_out);
     return hipGetLastError();
 }
 

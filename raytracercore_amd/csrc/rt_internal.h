@@ -72,7 +72,8 @@ struct alignas(16) FrameRec {
 // together by one slab test: the candidates are the face the ray enters by and the face it
 // leaves by, each kept under its face's culling rule and self-hit rule, entry first (a convex
 // box is met at most twice).  Faces f = 2 axis + side (side 0 = the lower plane) occupy slots
-// sg0 / 2 + f; their primitive IDs are id0 + (perm >> 4 f & 15).  Stored in the FrameRec array
+// sg0 / 2 + f (the kernels name a face by that slot); their primitive IDs are id0 + (perm >> 4 f & 15)
+// (kept for inspection).  Stored in the FrameRec array
 // (same 64-B size) so that the kernel needs no further argument.
 struct alignas(16) BoxRec {
     float4 lo;                  // xyz: lower planes, w = bitcast id0

@@ -127,13 +127,17 @@ hipError_t launch_accumulate(const PathParams& p, double* d_sum, uint32_t* d_sam
 // SampleSet.GetOutput over planar accumulators (row-major w*h) -> ARGB codes.
 hipError_t launch_tonemap(int w, int h, const double* d_sum, const uint32_t* d_samples, const uint32_t* d_misses,
                           rt_color back, double back_alpha, double exposure, int32_t* d_argb, hipStream_t stream);
-// planar row-major accumulators (w*h) -> DoubleColor rgb, samples and misses in x*h + y order
-// (the host-buffer entry point's layout).
+// One pixel of the host-buffer entry point's layout (rt_render_tile): the accumulated DoubleColor,
+// samples and misses, in the caller's x*h + y order.
+struct TileRec {
+    double r, g, b;
+    uint32_t samples, misses;
+};
+// planar row-major accumulators (w*h) -> TileRec[w*h] in x*h + y order
 hipError_t launch_tile_host_layout(int w, int h, const double* d_sum, const uint32_t* d_samples,
-                                  const uint32_t* d_misses, double* d_rgb, uint32_t* d_n, uint32_t* d_m,
-                                  hipStream_t stream);
-// partial (1 spp) -> DoubleColor[w, h] in x*h + y order, Placeholder(-1) on a miss.
-hipError_t launch_colors_1spp(const PathParams& p, double* d_out, hipStream_t stream);
+                                  const uint32_t* d_misses, TileRec* d_out, hipStream_t stream);
+// partial (1 spp) -> the DoubleColor[w, h] values as fp32 rgb in x*h + y order, Placeholder(-1) on a miss.
+hipError_t launch_colors_1spp(const PathParams& p, float* d_out, hipStream_t stream);
 
 #endif
 

@@ -194,7 +194,11 @@ struct rt_scene {
     DevBuf<unsigned long long> rays;
     DevBuf<float4> partial;
     DevBuf<double> sum, colors;
-    HostBuf<double> stage; // host-buffer entry points (rt_render_tile, rt_render_tile_1spp)
+    DevBuf<float> colors32;        // rt_render_tile_1spp: one pass as fp32 rgb in the caller's order
+    HostBuf<unsigned char> stage;  // host-buffer entry points (rt_render_tile, rt_render_tile_1spp)
+    HostBuf<unsigned long long> rays_h;
+    static constexpr int kCopyChunks = 8; // chunked device -> host copies (copy_consume)
+    std::array<hipEvent_t, kCopyChunks> copy_ev{};
     DevBuf<uint32_t> samples, misses;
     DevBuf<int32_t> ids;
     bool stats_on = false;      // launch the instrumented kernel (rt_scene_set_stats)
@@ -236,6 +240,8 @@ struct rt_scene {
         for (hipEvent_t e : slot_ev)
             if (e) (void)hipEventDestroy(e);
         if (done_ev) (void)hipEventDestroy(done_ev);
+        for (hipEvent_t e : copy_ev)
+            if (e) (void)hipEventDestroy(e);
         for (int i = 0; i < kTimeRing; i++) {
             if (t_start[i]) (void)hipEventDestroy(t_start[i]);
             if (t_end[i]) (void)hipEventDestroy(t_end[i]);
@@ -813,6 +819,98 @@ BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<
     return out;
 }
 
+// Materials, deduplicated: one MatF per distinct record, PrimF.d.w its index.  A 1M-triangle
+// mesh of one material then shades from a table of a few records (cache-resident) instead of
+// gathering 80 B per hit from an 80 MB per-primitive array.
+struct MatTable {
+    std::vector<MatF> mats;
+    std::vector<int32_t> mat_of; // per primitive ID
+};
+MatTable make_materials(const std::vector<HostPrim>& H, double air_ior)
+{
+    MatTable t;
+    const int n = (int)H.size();
+    t.mat_of.resize(n);
+    std::unordered_map<std::string, int32_t> mat_index;
+    for (int i = 0; i < n; i++) {
+        const HostPrim& p = H[i];
+        const bool refl = p.shininess > 0; // Primitive.IsReflective (Primitive.cs:107-129)
+        rt_color spec = refl ? p.specular : rt_color{0, 0, 0};
+        rt_color refr = refl ? p.refraction : rt_color{0, 0, 0};
+        MatF m;
+        std::memset(&m, 0, sizeof m);
+        m.emission = make_float4((float)p.emission.r, (float)p.emission.g, (float)p.emission.b, (float)luminance(p.emission));
+        m.diffuse = make_float4((float)p.diffuse.r, (float)p.diffuse.g, (float)p.diffuse.b, (float)luminance(p.diffuse));
+        m.specular = make_float4((float)spec.r, (float)spec.g, (float)spec.b, (float)luminance(spec));
+        m.refraction = make_float4((float)refr.r, (float)refr.g, (float)refr.b, (float)luminance(refr));
+        m.shininess = (float)p.shininess;
+        m.ior = (float)p.ior;
+        m.flags = p.flags;
+        m.inv_shininess = (float)(1.0 / p.shininess);
+        // Raytracer.cs:127-133: ratio = iorIn / iorOut, air outside, swapped when the hit is Inside
+        m.eta_enter = p.ior != 0 ? (float)(air_ior / p.ior) : 0.0f;
+        m.eta_exit = p.ior != 0 ? (float)(p.ior / air_ior) : 0.0f;
+        m.pad[0] = m.pad[1] = 0.0f;
+        const std::string key(reinterpret_cast<const char*>(&m), sizeof m);
+        auto it = mat_index.find(key);
+        if (it == mat_index.end()) {
+            it = mat_index.emplace(key, (int32_t)t.mats.size()).first;
+            t.mats.push_back(m);
+        }
+        t.mat_of[i] = it->second;
+    }
+    return t;
+}
+
+// The grouped order's groups sorted by the distance from the camera to their boxes (stable).
+std::vector<GroupRec> groups_nearest_first(std::vector<GroupRec> g, const CameraD& cam)
+{
+    const double px = cam.position.x, py = cam.position.y, pz = cam.position.z;
+    auto dist2 = [&](const GroupRec& G) {
+        // distance from the camera to the group's box (0 inside)
+        const double dx = std::max({0.0, (double)G.lo.x - px, px - (double)G.hi.x});
+        const double dy = std::max({0.0, (double)G.lo.y - py, py - (double)G.hi.y});
+        const double dz = std::max({0.0, (double)G.lo.z - pz, pz - (double)G.hi.z});
+        return dx * dx + dy * dy + dz * dz;
+    };
+    std::stable_sort(g.begin(), g.end(), [&](const GroupRec& a, const GroupRec& b) { return dist2(a) < dist2(b); });
+    return g;
+}
+
+// The fp32 transform rows of a transformed sphere (XformF).
+XformF make_xformf(const HostPrim& p)
+{
+    XformF F;
+    const double c[3] = {p.center.x, p.center.y, p.center.z};
+    for (int r = 0; r < 3; r++) {
+        F.to_world[r] = make_float4((float)p.to_world[4 * r], (float)p.to_world[4 * r + 1], (float)p.to_world[4 * r + 2],
+                                    (float)p.to_world[4 * r + 3]);
+        // normal(p) = N3 * (W * p + w - c) / r: one affine map of the world hit point
+        double row[4] = {0, 0, 0, 0};
+        for (int k = 0; k < 3; k++) {
+            const double nk = p.to_normal[4 * r + k] / p.radius;
+            for (int j = 0; j < 3; j++) row[j] += nk * p.to_world[4 * k + j];
+            row[3] += nk * (p.to_world[4 * k + 3] - c[k]);
+        }
+        F.normal[r] = make_float4((float)row[0], (float)row[1], (float)row[2], (float)row[3]);
+    }
+    return F;
+}
+
+// What the scene's primitives and materials use at all (FACT_*, rt_internal.h).
+uint32_t scene_facts(const std::vector<HostPrim>& H)
+{
+    uint32_t facts = 0;
+    for (const HostPrim& p : H) {
+        if (std::isinf(p.shininess) && p.shininess > 0) facts |= FACT_INF_SHININESS;
+        if ((float)p.ior != 0.0f) facts |= FACT_IOR;
+        if (p.flags & F_TRANSFORMED) facts |= FACT_XF;
+        if (p.flags & F_HASNORMALS) facts |= FACT_VN;
+        if (p.kind == RT_PRIM_SPHERE) facts |= FACT_SPHERE;
+    }
+    return facts;
+}
+
 int upload_scene(rt_scene* s)
 {
     const auto& H = s->host;
@@ -849,21 +947,7 @@ int upload_scene(rt_scene* s)
                 std::memcpy(X.to_obj, p.to_obj, sizeof X.to_obj);
                 std::memcpy(X.to_normal, p.to_normal, sizeof X.to_normal);
                 xd.push_back(X);
-                XformF F;
-                const double c[3] = {p.center.x, p.center.y, p.center.z};
-                for (int r = 0; r < 3; r++) {
-                    F.to_world[r] = make_float4((float)p.to_world[4 * r], (float)p.to_world[4 * r + 1],
-                                                (float)p.to_world[4 * r + 2], (float)p.to_world[4 * r + 3]);
-                    // normal(p) = N3 * (W * p + w - c) / r: one affine map of the world hit point
-                    double row[4] = {0, 0, 0, 0};
-                    for (int k = 0; k < 3; k++) {
-                        const double nk = p.to_normal[4 * r + k] / p.radius;
-                        for (int j = 0; j < 3; j++) row[j] += nk * p.to_world[4 * k + j];
-                        row[3] += nk * (p.to_world[4 * k + 3] - c[k]);
-                    }
-                    F.normal[r] = make_float4((float)row[0], (float)row[1], (float)row[2], (float)row[3]);
-                }
-                xf.push_back(F);
+                xf.push_back(make_xformf(p));
             }
         } else {
             d.a = p.pn;
@@ -888,47 +972,11 @@ int upload_scene(rt_scene* s)
         s->layout.tris = L.tris;
         s->layout.sphs = L.sphs;
     }
-    // Materials, deduplicated: one MatF per distinct record, PrimF.d.w its index.  A 1M-triangle
-    // mesh of one material then shades from a table of a few records (cache-resident) instead of
-    // gathering 80 B per hit from an 80 MB per-primitive array.
-    std::vector<MatF> mats;
-    std::vector<int32_t> mat_of(n);
-    std::unordered_map<std::string, int32_t> mat_index;
-    for (int i = 0; i < n; i++) {
-        const HostPrim& p = H[i];
-        const bool refl = p.shininess > 0; // Primitive.IsReflective (Primitive.cs:107-129)
-        rt_color spec = refl ? p.specular : rt_color{0, 0, 0};
-        rt_color refr = refl ? p.refraction : rt_color{0, 0, 0};
-        MatF m;
-        std::memset(&m, 0, sizeof m);
-        m.emission = make_float4((float)p.emission.r, (float)p.emission.g, (float)p.emission.b, (float)luminance(p.emission));
-        m.diffuse = make_float4((float)p.diffuse.r, (float)p.diffuse.g, (float)p.diffuse.b, (float)luminance(p.diffuse));
-        m.specular = make_float4((float)spec.r, (float)spec.g, (float)spec.b, (float)luminance(spec));
-        m.refraction = make_float4((float)refr.r, (float)refr.g, (float)refr.b, (float)luminance(refr));
-        m.shininess = (float)p.shininess;
-        m.ior = (float)p.ior;
-        m.flags = p.flags;
-        m.inv_shininess = (float)(1.0 / p.shininess);
-        // Raytracer.cs:127-133: ratio = iorIn / iorOut, air outside, swapped when the hit is Inside
-        m.eta_enter = p.ior != 0 ? (float)(s->params.air_ior / p.ior) : 0.0f;
-        m.eta_exit = p.ior != 0 ? (float)(p.ior / s->params.air_ior) : 0.0f;
-        m.pad[0] = m.pad[1] = 0.0f;
-        const std::string key(reinterpret_cast<const char*>(&m), sizeof m);
-        auto it = mat_index.find(key);
-        if (it == mat_index.end()) {
-            it = mat_index.emplace(key, (int32_t)mats.size()).first;
-            mats.push_back(m);
-        }
-        mat_of[i] = it->second;
-    }
-    uint32_t facts = 0;
-    for (const HostPrim& p : H) {
-        if (std::isinf(p.shininess) && p.shininess > 0) facts |= FACT_INF_SHININESS;
-        if ((float)p.ior != 0.0f) facts |= FACT_IOR;
-        if (p.flags & F_TRANSFORMED) facts |= FACT_XF;
-        if (p.flags & F_HASNORMALS) facts |= FACT_VN;
-        if (p.kind == RT_PRIM_SPHERE) facts |= FACT_SPHERE;
-    }
+    // Materials, deduplicated (make_materials), and the scene facts
+    const MatTable mt = make_materials(H, s->params.air_ior);
+    const std::vector<MatF>& mats = mt.mats;
+    const std::vector<int32_t>& mat_of = mt.mat_of;
+    uint32_t facts = scene_facts(H);
     if (getenv("RTCORE_NO_FACTS")) facts = FACT_ALL; // A/B: every shading feature compiled in
     auto set_mats = [&](std::vector<PrimF>& v) { // PrimF.d.w = the material of the record's ID
         for (PrimF& f : v) {
@@ -1521,6 +1569,47 @@ int end_op(rt_scene* s, hipStream_t stream)
     return RT_OK;
 }
 
+// The host-buffer entry points' device -> host step: n_items records of rec_bytes from d_src (queued
+// after the render on the scene's stream) into pinned staging in up to kCopyChunks chunks, each
+// chunk's arrival recorded by an event, and consume(stage, a, b) on the host pool for item ranges
+// [a, b) as soon as their chunk has landed, so that the host pass over one chunk overlaps the DMA of
+// the next.  Returns when every item is consumed.
+int copy_consume(rt_scene* s, const void* d_src, size_t n_items, size_t rec_bytes,
+                 const std::function<void(const unsigned char*, size_t, size_t)>& consume)
+{
+    const size_t bytes = n_items * rec_bytes;
+    HIP_TRY(s->stage.reserve(bytes));
+    const size_t K = std::max<size_t>(1, std::min<size_t>(rt_scene::kCopyChunks, bytes >> 20)); // >= 1 MB per chunk
+    const size_t per = (n_items + K - 1) / K;
+    for (size_t k = 0; k < K; k++) {
+        const size_t a = std::min(n_items, k * per), b = std::min(n_items, (k + 1) * per);
+        if (!s->copy_ev[k]) HIP_TRY(hipEventCreateWithFlags(&s->copy_ev[k], hipEventDisableTiming));
+        if (b > a)
+            HIP_TRY(hipMemcpyAsync(s->stage.p + a * rec_bytes, static_cast<const unsigned char*>(d_src) + a * rec_bytes,
+                                   (b - a) * rec_bytes, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipEventRecord(s->copy_ev[k], s->stream));
+    }
+    // K chunks x S slices, handed out in order: the first tasks wait for the first chunk
+    const size_t S = (size_t)host_threads();
+    std::atomic<int> failed{0};
+    host_run(K * S, [&](size_t t) {
+        const size_t k = t / S, j = t % S;
+        const size_t a0 = std::min(n_items, k * per), b0 = std::min(n_items, (k + 1) * per);
+        const size_t sl = (b0 - a0 + S - 1) / S;
+        const size_t a = std::min(b0, a0 + j * sl), b = std::min(b0, a + sl);
+        if (hipEventSynchronize(s->copy_ev[k]) != hipSuccess) {
+            failed = 1;
+            return;
+        }
+        if (b > a) consume(s->stage.p, a, b);
+    });
+    if (failed) {
+        set_error("copy_consume: device -> host copy failed");
+        return RT_ERR_HIP;
+    }
+    return RT_OK;
+}
+
 } // namespace
 
 extern "C" {
@@ -1684,6 +1773,75 @@ int rt_debug_flat_records(const rt_prim* prims, int32_t n_prims, uint32_t* out, 
         return RT_ERR_ARG;
     }
     return RT_OK;
+}
+
+// Experiment support (host only, no device): the generated header of the scene-specialised build
+// that rt_scene_create + rt_scene_set_camera would make for these primitives and this camera, so
+// that its code can be compiled and read on a machine without a GPU (tools/jit_isa.py).  Returns
+// the header's length (copied into buf, NUL-terminated, when it fits in cap).
+int rt_debug_jit_header(const rt_scene_params* params, const rt_prim* prims, int32_t n_prims, const rt_camera* camera,
+                        int32_t grouped, char* buf, int64_t cap)
+{
+    if (!params || !camera || n_prims < 0 || (n_prims > 0 && !prims) || (grouped != 0 && grouped != 1)) {
+        set_error("rt_debug_jit_header: bad argument");
+        return RT_ERR_ARG;
+    }
+    const std::vector<HostPrim> H = prepare_prims(prims, n_prims);
+    const int n = (int)H.size();
+    std::vector<int> xf_index(n, -1);
+    std::vector<XformF> xf;
+    int nb = 0, np = 0, n_vn = 0;
+    for (int i = 0; i < n; i++) {
+        nb += H[i].kind != RT_PRIM_PLANE;
+        np += H[i].kind == RT_PRIM_PLANE;
+        n_vn += (H[i].kind == RT_PRIM_TRIANGLE && (H[i].flags & F_HASNORMALS)) ? 1 : 0;
+        if (H[i].kind == RT_PRIM_SPHERE && (H[i].flags & F_TRANSFORMED)) {
+            xf_index[i] = (int)xf.size();
+            xf.push_back(make_xformf(H[i]));
+        }
+    }
+    if (nb > 48) {
+        set_error("rt_debug_jit_header: the scene-specialised build serves brute-force scenes (<= 48 primitives)");
+        return RT_ERR_ARG;
+    }
+    const SahBvh sah = nb > 0 ? build_sah_bvh(H, n > 256 ? 3 : 2) : SahBvh{}; // as build_bvhs
+    const BruteOrders o = make_brute_orders(H, xf_index, sah);
+    const BruteOrder& B = grouped ? o.grouped : o.flat;
+    if (grouped && B.groups.empty()) {
+        set_error("rt_debug_jit_header: no grouped order for this scene");
+        return RT_ERR_ARG;
+    }
+    PathScene ps; // make_path_scene + fill_launch, from the host records
+    std::memset(&ps, 0, sizeof ps);
+    for (int k = 0; k < 3; k++) ps.n_rect[k] = o.nr[k];
+    ps.n_tri = o.nt;
+    ps.n_sph = o.ns;
+    ps.n_pln = np;
+    ps.n_bvh = (int)B.prims.size() - np;
+    ps.n_slots = ps.n_bvh + np;
+    ps.n_mats = (int)make_materials(H, params->air_ior).mats.size();
+    ps.n_xf = (int)xf.size();
+    ps.n_vn = n_vn;
+    ps.facts = getenv("RTCORE_NO_FACTS") ? (uint32_t)FACT_ALL : scene_facts(H);
+    ps.n_groups = grouped ? (int)B.groups.size() : 1;
+    ps.root = nb > 0 ? sah.root : 0;
+    ps.width = params->width;
+    ps.recursion = params->recursion;
+    ps.debug_geom = params->debug_geom;
+    const rt_color& a = params->ambient;
+    ps.ambient_miss = (a.r == -1 && a.g == -1 && a.b == -1) ? 1 : 0;
+    ps.air_ior = (float)params->air_ior;
+    ps.ambient_r = (float)a.r;
+    ps.ambient_g = (float)a.g;
+    ps.ambient_b = (float)a.b;
+    CameraD camd;
+    CameraF camf;
+    camera_init(*camera, params->width, params->height, camd, camf);
+    const std::vector<GroupRec> groups =
+        (grouped && B.groups.size() > 1 && !getenv("RTCORE_NO_GROUP_SORT")) ? groups_nearest_first(B.groups, camd) : B.groups;
+    const std::string h = jit_scene_header(ps, camf, grouped == 1, groups, B.rects, B.frames, B.tests, xf);
+    if (buf && cap > (int64_t)h.size()) std::memcpy(buf, h.c_str(), h.size() + 1);
+    return (int)h.size();
 }
 
 int rt_set_jit(int32_t on)
@@ -2101,16 +2259,7 @@ int rt_scene_set_camera(rt_scene* s, const rt_camera* cam)
     // early and skip the primitives of groups behind it (each group owns its own ranges, so only
     // the GroupRec order changes).  Deterministic for a given scene and camera.
     if (s->groups_gr_host.size() > 1 && !getenv("RTCORE_NO_GROUP_SORT")) {
-        std::vector<GroupRec> g = s->groups_gr_host;
-        const double px = s->camd.position.x, py = s->camd.position.y, pz = s->camd.position.z;
-        auto dist2 = [&](const GroupRec& G) {
-            // distance from the camera to the group's box (0 inside)
-            const double dx = std::max({0.0, (double)G.lo.x - px, px - (double)G.hi.x});
-            const double dy = std::max({0.0, (double)G.lo.y - py, py - (double)G.hi.y});
-            const double dz = std::max({0.0, (double)G.lo.z - pz, pz - (double)G.hi.z});
-            return dx * dx + dy * dy + dz * dz;
-        };
-        std::stable_sort(g.begin(), g.end(), [&](const GroupRec& a, const GroupRec& b) { return dist2(a) < dist2(b); });
+        const std::vector<GroupRec> g = groups_nearest_first(s->groups_gr_host, s->camd);
         HIP_TRY(hipMemcpy(s->groups_gr.p, g.data(), g.size() * sizeof(GroupRec), hipMemcpyHostToDevice));
         s->grouped_h.groups = g; // the order the scene-specialised grouped kernel is built with
     }
@@ -2266,30 +2415,26 @@ int rt_render_tile(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, in
     rc = rt_render_device(s, x0, y0, w, h, spp, seed, sample_base, s->sum.p, s->samples.p, s->misses.p, s->rays.p,
                           s->stream);
     if (rc != RT_OK) return rc;
-    // the caller's layout on the device, one contiguous copy into pinned staging, then a parallel
-    // sequential add (a strided single-threaded transpose on the host took ~30 ms at 1080p)
-    HIP_TRY(s->colors.reserve(4 * npix)); // rgb (3 doubles) + samples and misses (2 x u32) per pixel
-    HIP_TRY(s->stage.reserve(4 * npix));
-    double* d_rgb = s->colors.p;
-    uint32_t* d_nm = reinterpret_cast<uint32_t*>(s->colors.p + 3 * npix);
-    HIP_TRY(launch_tile_host_layout(w, h, s->sum.p, s->samples.p, s->misses.p, d_rgb, d_nm, d_nm + npix, s->stream));
-    unsigned long long hr = 0;
-    HIP_TRY(hipMemcpyAsync(s->stage.p, s->colors.p, 4 * npix * sizeof(double), hipMemcpyDeviceToHost, s->stream));
-    HIP_TRY(hipMemcpyAsync(&hr, s->rays.p, sizeof hr, hipMemcpyDeviceToHost, s->stream));
-    HIP_TRY(hipStreamSynchronize(s->stream));
-    const double* hs = s->stage.p;
-    const uint32_t* hn = reinterpret_cast<const uint32_t*>(s->stage.p + 3 * npix);
-    const uint32_t* hm = hn + npix;
-    parallel_ranges(npix, 65536, [&](size_t a, size_t b) {
+    // the caller's layout on the device (one 32-B TileRec per pixel, x*h + y), copied in chunks into
+    // pinned staging and added into the caller's arrays chunk by chunk as the chunks land
+    // (copy_consume; a strided single-threaded transpose on the host took ~30 ms at 1080p)
+    HIP_TRY(s->colors.reserve(4 * npix)); // 32 B per pixel
+    HIP_TRY(s->rays_h.reserve(1));
+    TileRec* d_rec = reinterpret_cast<TileRec*>(s->colors.p);
+    HIP_TRY(launch_tile_host_layout(w, h, s->sum.p, s->samples.p, s->misses.p, d_rec, s->stream));
+    HIP_TRY(hipMemcpyAsync(s->rays_h.p, s->rays.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
+    rc = copy_consume(s, d_rec, npix, sizeof(TileRec), [&](const unsigned char* st, size_t a, size_t b) {
+        const TileRec* r = reinterpret_cast<const TileRec*>(st);
         for (size_t o = a; o < b; o++) {
-            sum_rgb[o].r += hs[3 * o + 0];
-            sum_rgb[o].g += hs[3 * o + 1];
-            sum_rgb[o].b += hs[3 * o + 2];
-            samples[o] += hn[o];
-            misses[o] += hm[o];
+            sum_rgb[o].r += r[o].r;
+            sum_rgb[o].g += r[o].g;
+            sum_rgb[o].b += r[o].b;
+            samples[o] += r[o].samples;
+            misses[o] += r[o].misses;
         }
     });
-    if (rays_out) *rays_out += hr;
+    if (rc != RT_OK) return rc;
+    if (rays_out) *rays_out += s->rays_h.p[0]; // copied before the chunks, on the same stream
     return RT_OK;
 }
 
@@ -2304,20 +2449,20 @@ int rt_render_tile_1spp(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t 
     }
     HIP_TRY(hipSetDevice(s->device));
     const size_t npix = (size_t)w * h;
-    HIP_TRY(s->colors.reserve(3 * npix));
+    HIP_TRY(s->colors32.reserve(3 * npix));
     HIP_TRY(hipMemsetAsync(s->rays.p, 0, sizeof(unsigned long long), s->stream));
     PathParams p = make_params(s, x0, y0, w, h, 1, seed, sample_index);
     rc = run_path(s, p, s->rays.p, s->stream);
     if (rc != RT_OK) return rc;
-    HIP_TRY(launch_colors_1spp(p, s->colors.p, s->stream));
+    // the pass as fp32 in the caller's order (the kernel's sample values are fp32: widened exactly
+    // on the host), 12 B per pixel over PCIe instead of 24, in chunks widened as they land
+    HIP_TRY(launch_colors_1spp(p, s->colors32.p, s->stream));
     rc = end_op(s, s->stream);
     if (rc != RT_OK) return rc;
-    HIP_TRY(s->stage.reserve(3 * npix));
-    HIP_TRY(hipMemcpyAsync(s->stage.p, s->colors.p, npix * sizeof(rt_color), hipMemcpyDeviceToHost, s->stream));
-    HIP_TRY(hipStreamSynchronize(s->stream));
-    const double* src = s->stage.p;
-    parallel_ranges(npix, 65536, [&](size_t a, size_t b) { std::memcpy(out + a, src + 3 * a, (b - a) * sizeof(rt_color)); });
-    return RT_OK;
+    return copy_consume(s, s->colors32.p, npix, 3 * sizeof(float), [&](const unsigned char* st, size_t a, size_t b) {
+        const float* f = reinterpret_cast<const float*>(st);
+        for (size_t o = a; o < b; o++) out[o] = rt_color{(double)f[3 * o], (double)f[3 * o + 1], (double)f[3 * o + 2]};
+    });
 }
 
 } // extern "C"

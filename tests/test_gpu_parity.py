@@ -147,6 +147,34 @@ def test_host_tile_equals_device_render_1080p(rc, scenes):
     gpu.close()
 
 
+@pytest.mark.parametrize("tile", [(0, 0, 1920, 1080), (3, 5, 1001, 777)])
+def test_one_pass_equals_device_render(rc, scenes, tile):
+    """rt_render_tile_1spp (Raytracer.Render's one pass, copied in chunks as fp32 and widened on the
+    host) equals the device-resident 1-spp render of the same sample: the colour where the sample
+    hit, Placeholder (-1) where it missed, bit for bit; a whole 1080p frame and a ragged tile whose
+    pixel count splits unevenly over the copy chunks."""
+    import torch
+
+    x0, y0, w, h = tile
+    gpu = rc.GpuRaytracer(scenes["bounce.txt"], 0, size=(1920, 1080))
+    dev = torch.device("cuda", 0)
+    d_sum = torch.zeros(3 * w * h, dtype=torch.float64, device=dev)
+    d_n = torch.zeros(w * h, dtype=torch.int32, device=dev)
+    d_m = torch.zeros(w * h, dtype=torch.int32, device=dev)
+    d_r = torch.zeros(1, dtype=torch.int64, device=dev)
+    gpu.render_device(x0, y0, w, h, 1, 9, 41, d_sum.data_ptr(), d_n.data_ptr(), d_m.data_ptr(), d_r.data_ptr(), 0)
+    torch.cuda.synchronize(dev)
+    ds = d_sum.cpu().numpy().reshape(3, h, w).transpose(2, 1, 0)  # -> [x, y, rgb]
+    miss = (d_m.cpu().numpy().reshape(h, w).T == 1)
+    want = np.where(miss[..., None], -1.0, ds)
+    buf = np.full((w, h, 3), 7.0)
+    for _ in range(2):  # into a reused array, twice (no accumulation: the pass overwrites)
+        got = gpu.render_tile_1spp(x0, y0, w, h, seed=9, sample_index=41, out=buf)
+        assert got is buf and np.array_equal(got, want)
+    assert np.array_equal(gpu.render_tile_1spp(x0, y0, w, h, seed=9, sample_index=41), want)
+    gpu.close()
+
+
 def test_full_1080p_properties(rc, scenes):
     """Full configs[1] workload: bookkeeping, reproducibility, rays per sample."""
     import torch

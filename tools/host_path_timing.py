@@ -1,11 +1,17 @@
 """Rates through the host-buffer entry points (the PCIe-inclusive view; bench.py's `value` keeps the
 accumulators in HBM): rt_render_tile (spp samples per call into host SampleSet buffers) and
 rt_render_tile_1spp (Raytracer.Render's one-pass contract, DoubleColor[w, h] per pass), 1080p
-bounce.txt camera 0.  Prints one JSON line."""
+bounce.txt camera 0.  Prints one JSON line.
+
+The one-pass figure is taken into one reused output array (a C# caller's pinned DoubleColor[w, h],
+zeroed by the runtime, has its pages mapped); `render_tile_1spp_fresh` allocates a new numpy array
+per pass, whose first-touch page faults the call then pays."""
 import json
 import os
 import sys
 import time
+
+import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import raytracercore_amd as rc  # noqa: E402
@@ -25,13 +31,16 @@ for spp in (256, 16):
     dt = (time.perf_counter() - t0) / n
     out[f"render_tile_{spp}spp"] = {"ms_per_call": round(dt * 1e3, 2), "mrays_per_s": round(rays / n / dt / 1e6, 1),
                                    "kernel_ms": round(g.last_kernel_ms(), 2)}
-g.render_tile_1spp(0, 0, W, H, seed=1, sample_index=0)
-t0 = time.perf_counter()
-n = 20
-for k in range(n):
-    g.render_tile_1spp(0, 0, W, H, seed=1, sample_index=k + 1)
-dt = (time.perf_counter() - t0) / n
-out["render_tile_1spp"] = {"ms_per_pass": round(dt * 1e3, 2), "msamples_per_s": round(W * H / dt / 1e6, 1),
-                           "kernel_ms": round(g.last_kernel_ms(), 2)}
+buf = np.zeros((W, H, 3), np.float64)
+g.render_tile_1spp(0, 0, W, H, seed=1, sample_index=0, out=buf)
+for label, reuse in (("render_tile_1spp", True), ("render_tile_1spp_fresh", False)):
+    n = 40
+    t0 = time.perf_counter()
+    for k in range(n):
+        g.render_tile_1spp(0, 0, W, H, seed=1, sample_index=k + 1, out=buf if reuse else None)
+    dt = (time.perf_counter() - t0) / n
+    kt = g.kernel_times(min(n, g.KERNEL_TIME_RING))
+    out[label] = {"ms_per_pass": round(dt * 1e3, 3), "msamples_per_s": round(W * H / dt / 1e6, 1),
+                  "kernel_ms": round(float(np.mean(kt)), 3)}
 g.close()
 print(json.dumps(out), flush=True)
