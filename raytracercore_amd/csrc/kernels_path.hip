@@ -789,16 +789,29 @@ __device__ __forceinline__ int shade(const SceneT& s, const PrimF* __restrict__ 
         return 1;
     }
     // hit position and normal facing the incoming ray: one straight-line form for every kind
-    // (world point o + t d; flat kinds carry their face normal in P.d, spheres 1/r in P.b.y), with
-    // transformed spheres and vertex-normal triangles on a separate (rare) path
+    // (world point o + t d), with transformed spheres and vertex-normal triangles on a separate
+    // (rare) path.  The rectangle tests do not track the side of their hit, so a rectangle's
+    // Inside is recomputed here (Moller-Trumbore's inside = d . N > 0), and an axis-aligned one's
+    // hit point is put on its plane.
     V3 pos = madd(S.d, b.t, S.o);
     const bool sph = (s.facts & FACT_SPHERE) && kind == RT_PRIM_SPHERE;
-    const uint32_t axis = (fl & F_AXIS_MASK) >> F_AXIS_SHIFT; // axis-aligned rectangle: on its plane
-    if (axis | (fl & F_FRAME_RECT)) gin = dot(S.d, xyz(P.d)) > 0.0f; // Moller-Trumbore's inside = d . N > 0
-    pos.x = axis == 1 ? P.a.x : pos.x;
-    pos.y = axis == 2 ? P.a.y : pos.y;
-    pos.z = axis == 3 ? P.a.z : pos.z;
-    V3 n = sph ? (pos - xyz(P.a)) * P.b.y : xyz(P.d);
+    V3 n;
+    if (SLOT) { // the BVH kernels (records in global memory: the three rows a, b, d only)
+        const uint32_t axis = (fl & F_AXIS_MASK) >> F_AXIS_SHIFT; // axis-aligned rectangle: on its plane
+        if (axis | (fl & F_FRAME_RECT)) gin = dot(S.d, xyz(P.d)) > 0.0f;
+        pos.x = axis == 1 ? P.a.x : pos.x;
+        pos.y = axis == 2 ? P.a.y : pos.y;
+        pos.z = axis == 3 ? P.a.z : pos.z;
+        n = sph ? (pos - xyz(P.a)) * P.b.y : xyz(P.d);
+    } else { // the brute-force kernels (records in LDS): the same by arithmetic on the shading row c
+        // c.xyz: one-hot plane axis of an axis-aligned rectangle (the hit point moves onto the plane
+        // through v0 = P.a), c.w: 1/r of a sphere, whose P.d holds -centre/r (normal = p/r - c/r), 0
+        // for the flat kinds, whose P.d is the face normal
+        const float4 Pc = prims[b.sg >> 1].c;
+        pos = v3(fmaf(Pc.x, P.a.x - pos.x, pos.x), fmaf(Pc.y, P.a.y - pos.y, pos.y), fmaf(Pc.z, P.a.z - pos.z, pos.z));
+        n = madd(pos, Pc.w, xyz(P.d));
+        if (fl & (F_AXIS_MASK | F_FRAME_RECT)) gin = dot(S.d, xyz(P.d)) > 0.0f;
+    }
     float bu = 0.0f, bv = 0.0f; // vertex-normal triangle: the barycentrics of the hit
     if ((s.facts & (FACT_XF | FACT_VN)) && (fl & (F_TRANSFORMED | F_HASNORMALS))) {
         if (sph) { // ellipsoid: the world normal is an affine map of the world hit point

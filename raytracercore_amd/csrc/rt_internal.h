@@ -115,8 +115,9 @@ struct alignas(16) RefNode {    // 80 B, depth-first pre-order; left child = thi
 struct alignas(16) PrimF {      // 64 B
     float4 a; // tri: v0.xyz, id | sphere: c.xyz, id | plane: N.xyz, id
     float4 b; // tri: e01.xyz, flags | sphere: (r, 1/r, xf, flags) | plane: (dist, 0, 0, flags)
-    float4 c; // tri: e02.xyz, 0
-    float4 d; // tri and plane: N.xyz, 0
+    float4 c; // the brute-force kernels' shading row: one-hot plane axis of an axis-aligned rectangle
+              // slot (xyz), 1/r of an untransformed sphere (w); 0 otherwise
+    float4 d; // tri and plane: N.xyz | untransformed sphere: -centre / r; w: material index
 };
 
 struct alignas(16) XformF {     // rows 0-2 (last row is 0 0 0 1)

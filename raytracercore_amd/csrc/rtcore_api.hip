@@ -115,6 +115,14 @@ float as_f(uint32_t v)
 }
 double luminance(rt_color c) { return 0.299 * c.r + 0.587 * c.g + 0.114 * c.b; } // DoubleColor.cs:76-79
 uint32_t p_flags_with_axis(uint32_t flags, int axis) { return flags | ((uint32_t)(axis + 1) << F_AXIS_SHIFT); }
+// A slot tested as an axis-aligned rectangle on plane `axis`: its flags name the axis, and its
+// shading row c (brute-force kernels) the one-hot axis whose hit coordinate is the plane's.
+void set_rect_axis(PrimF& f, uint32_t flags, int axis)
+{
+    const uint32_t fl = p_flags_with_axis(flags, axis);
+    std::memcpy(&f.b.w, &fl, 4);
+    f.c = make_float4(axis == 0 ? 1.0f : 0.0f, axis == 1 ? 1.0f : 0.0f, axis == 2 ? 1.0f : 0.0f, 0.0f);
+}
 
 } // namespace
 
@@ -261,11 +269,16 @@ PrimF make_primf(const std::vector<HostPrim>& H, const std::vector<int>& xf_inde
         if (p.kind == RT_PRIM_TRIANGLE) {
             f.a = f4(p.v[0], as_f(i));
             f.b = f4(p.e01, as_f(p.flags));
-            f.c = f4(p.e02, 0.0f);
+            f.c = make_float4(0.0f, 0.0f, 0.0f, 0.0f); // the shading row (see set_rect_axis)
             f.d = f4(p.n, 0.0f);
         } else if (p.kind == RT_PRIM_SPHERE) {
             f.a = f4(p.center, as_f(i));
             f.b = make_float4((float)p.radius, (float)(1.0 / p.radius), as_f(xf_index[i]), as_f(p.flags));
+            if (!(p.flags & F_TRANSFORMED)) { // brute-force shading: normal = p / r - centre / r
+                const double ir = 1.0 / p.radius;
+                f.c = make_float4(0.0f, 0.0f, 0.0f, (float)ir);
+                f.d = make_float4((float)(-p.center.x * ir), (float)(-p.center.y * ir), (float)(-p.center.z * ir), 0.0f);
+            }
         } else {
             f.a = f4(p.pn, as_f(i));
             f.b = make_float4((float)p.pd, 0.0f, 0.0f, as_f(p.flags));
@@ -636,8 +649,7 @@ BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<
                     if (wused[j] || wr[j].k != kind) continue;
                     const int i = wr[j].i;
                     PrimF f = primf(i);
-                    const uint32_t fl = p_flags_with_axis(H[i].flags, kind);
-                    std::memcpy(&f.b.w, &fl, 4);
+                    set_rect_axis(f, H[i].flags, kind);
                     o.rects.push_back(rectrec(i, kind));
                     o.rects.back().sg = (int)o.prims.size() << 1;
                     o.nr[kind]++;
@@ -710,8 +722,7 @@ BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<
                 for (int fi = 0; fi < 6; fi++) {
                     const int i = box_face_prim(wr, f6, fi), kind = fi >> 1;
                     PrimF f = primf(i);
-                    const uint32_t fl = p_flags_with_axis(H[i].flags, kind);
-                    std::memcpy(&f.b.w, &fl, 4);
+                    set_rect_axis(f, H[i].flags, kind);
                     push_slot(i, f);
                     G.n_flat_extra += f6.f[fi] >= 0;
                     o.nr[kind]++;
@@ -1232,7 +1243,9 @@ int resolve_traversal(rt_scene* s)
     const int plain = path_variant(kernel, false), staged = path_variant(kernel, true);
     const int occ_plain = path_blocks_per_cu(plain, path_dyn_lds(s->dev, plain), false, s->dev.n_vn > 0);
     const int occ_staged = lds <= 64 * 1024 ? path_blocks_per_cu(staged, path_dyn_lds(s->dev, staged), false, s->dev.n_vn > 0) : 0;
-    bool use_lds = occ_staged >= occ_plain;
+    // The scene-specialised build (rt_set_jit) is a build of the staged brute-force variant, and its
+    // occupancy is its own: with it on, a brute-force order stays staged whenever the records fit.
+    bool use_lds = occ_staged >= occ_plain || (kernel <= 1 && occ_staged > 0 && jit_enabled());
     if (const char* e = getenv("RTCORE_PATH_LDS")) use_lds = e[0] == '1' && occ_staged > 0;
     s->variant = use_lds ? staged : plain;
     s->blocks_per_cu = use_lds ? occ_staged : occ_plain;

@@ -243,6 +243,34 @@ def test_scene_specialised_build_compiles(rc, grouped):
     assert rc.jit_compile_check("gfx950", grouped) > 1000
 
 
+@pytest.mark.parametrize("name,grouped", [("bounce.txt", False), ("die.txt", True)])
+def test_scene_specialised_header_of_shipped_scenes(rc, name, grouped, tmp_path):
+    """rt_debug_jit_header (host only): the generated header of the shipped scenes' specialised
+    builds.  The flat order's carries only the camera's kind and depth-of-field switch (one build
+    serves every camera of those), the grouped order's the camera itself; both compile for gfx950
+    with the embedded sources (tools/jit_isa.py, the run-time build's options)."""
+    import subprocess
+    import sys
+
+    scene = rc.SceneLoader.from_file(rc.scene_path(name))
+    h = rc.jit_header(scene, 0, size=(1920, 1080), grouped=grouped)
+    assert "kSceneW" in h and "kRectsW" in h
+    if grouped:
+        assert "#define RT_SCENE_CONST_CAMERA 1" in h and "kCameraW" in h
+    else:
+        assert "#define RT_SCENE_CONST_CAMERA 0" in h and "kCameraW" not in h
+        assert "#define RT_SCENE_CAMERA_KIND 0" in h and "#define RT_SCENE_CAMERA_DOF 0" in h
+        # another camera of the same kind: the same header, so no new build
+        assert rc.jit_header(scene, 1, size=(1920, 1080)) == h
+    hdr = tmp_path / "hdr.h"
+    hdr.write_text(h)
+    tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "jit_isa.py")
+    out = subprocess.run([sys.executable, tool, str(hdr), "1" if grouped else "0", str(tmp_path / "k")],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "rt_path_const" in (tmp_path / "k.s").read_text()
+
+
 def test_vertexnormal_rehit_test_matches_oracle(rc):
     """The kernels' fp64 re-hit test of a vertex-normal triangle (rt_debug_vn_rehit, the host build of
     vn_rehit_test) against the oracle's own Triangle.RayTraceAVXFaster restatement on
