@@ -6,7 +6,7 @@ import os
 import subprocess
 import sys
 
-CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "raytracercore_amd", "csrc")
+CSRC = os.environ.get("RTCORE_CSRC") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "raytracercore_amd", "csrc")
 NAMES = ["rt_jit_prelude.h", "kernels_path.hip", "../../include/rtcore_rng.h", "rt_kernels.h", "rt_internal.h",
          "../../include/rtcore.h"]
 
