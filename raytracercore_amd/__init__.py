@@ -176,6 +176,8 @@ def load_library(path: str = "") -> C.CDLL:
                                           C.c_void_p, P(C.c_float)]),
     }
     for name, (res, args) in sig.items():
+        if name.startswith("rt_debug_") and not hasattr(lib, name):
+            continue  # an older build (RTCORE_LIB, A/B measurements) without a newer debug entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -526,7 +526,9 @@ __device__ __forceinline__ void wide_visit(const Node4Q& q, V3 id, V3 oi, float 
         const float tmax = fminf(fminf(fmaf(ubyte(fx, K), ax, bx), fmaf(ubyte(fy, K), ay, by)),                   \
                                  fmaf(ubyte(fz, K), az, bz));                                                      \
         D = ((K < nc) & (tmin <= fminf(tmax * 1.00000024f, tmax_best))) ? tmin : __builtin_huge_valf();         \
-    } // (K < nc) without short-circuit: "&&" made each child a divergent branch
+    } // (K < nc) without short-circuit: "&&" made each child a divergent branch.  The test stays although
+      // an empty slot's box is inverted (quantize_node4): inverted only up to the fp32 rounding of the
+      // planes, and a hit on an empty slot would push RT_NODE4_EMPTY (round 4: dropping it saved 0.6 %)
     RT_WIDE_CHILD(0, d0)
     RT_WIDE_CHILD(1, d1)
     RT_WIDE_CHILD(2, d2)

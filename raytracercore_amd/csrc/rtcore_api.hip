@@ -1451,8 +1451,9 @@ int prepare_jit(rt_scene* s)
     // order's only the camera's kind and depth-of-field switch, so moving the camera among cameras
     // of one kind (MainWindow.cs:262-269 restarts the render with another scene camera) reuses the
     // build: the same header, no hiprtc build and no cache lookup.
+    static const bool cam_in = getenv("RTCORE_JIT_CAMERA") && getenv("RTCORE_JIT_CAMERA")[0] == '1'; // A/B: round 3's form
     const std::string header =
-        jit_scene_header(lp.scene, s->camf, grouped, B.groups, B.rects, B.frames, B.tests, s->xf_h);
+        jit_scene_header(lp.scene, s->camf, grouped || cam_in, B.groups, B.rects, B.frames, B.tests, s->xf_h);
     if (s->jit.variant == s->variant && s->jit.fn && header == s->jit.header) {
         s->jit.gen = gen;
         s->jit.status = 1;

@@ -271,6 +271,21 @@ def test_scene_specialised_header_of_shipped_scenes(rc, name, grouped, tmp_path)
     assert "rt_path_const" in (tmp_path / "k.s").read_text()
 
 
+def test_experiment_patches_apply():
+    """Cost experiments live in tools/exp_patch.py, not in the product kernel: every patch's anchors
+    occur exactly once in kernels_path.hip, and the kernel holds no experiment switches."""
+    import importlib.util
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("exp_patch", os.path.join(root, "tools", "exp_patch.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    src = open(os.path.join(root, "raytracercore_amd", "csrc", "kernels_path.hip")).read()
+    assert "RT_EXP_" not in src and "exp_sink" not in src
+    for name in mod.PATCHES:
+        assert mod.apply(src, [name]) != src, name
+
+
 def test_vertexnormal_rehit_test_matches_oracle(rc):
     """The kernels' fp64 re-hit test of a vertex-normal triangle (rt_debug_vn_rehit, the host build of
     vn_rehit_test) against the oracle's own Triangle.RayTraceAVXFaster restatement on
