@@ -1253,7 +1253,8 @@ int resolve_traversal(rt_scene* s)
     return RT_OK;
 }
 
-PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint64_t seed, uint64_t base);
+PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint64_t seed, uint64_t base,
+                       double chunk_npix = 0.0);
 int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t stream, bool timed = true);
 int prepare_jit(rt_scene* s);
 int end_op(rt_scene* s, hipStream_t stream);
@@ -1307,7 +1308,11 @@ int calibrate_grouping(rt_scene* s)
     return resolve_traversal(s);
 }
 
-PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint64_t seed, uint64_t base)
+// chunk_npix (default w * h): the pixel count the chunks per pixel are chosen for.  A column band of a
+// tile passes the whole tile's, so that every pixel's samples fall into the same chunks (and its
+// fp64 sum into the same order) as in one launch over the tile.
+PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint64_t seed, uint64_t base,
+                       double chunk_npix)
 {
     PathParams p{};
     p.x0 = x0;
@@ -1327,7 +1332,7 @@ PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint6
     // costs little, and the tail of a launch of long, divergent BVH paths shrinks.
     const int base_chunks = (s->variant >> 1) >= 2 ? 64 : 32;
     int chunks = base_chunks;
-    const double npix = (double)w * (double)h;
+    const double npix = chunk_npix > 0.0 ? chunk_npix : (double)w * (double)h;
     if (npix > 0 && npix < 2073600.0)
         chunks = (int)std::min(8.0 * base_chunks, base_chunks * std::ceil(2073600.0 / npix));
     // A larger frame has more items, so a relatively shorter tail: fewer, longer items then save
@@ -1583,32 +1588,44 @@ int end_op(rt_scene* s, hipStream_t stream)
     return RT_OK;
 }
 
-// The host-buffer entry points' device -> host step: n_items records of rec_bytes from d_src (queued
-// after the render on the scene's stream) into pinned staging in up to kCopyChunks chunks, each
-// chunk's arrival recorded by an event, and consume(stage, a, b) on the host pool for item ranges
-// [a, b) as soon as their chunk has landed, so that the host pass over one chunk overlaps the DMA of
-// the next.  Returns when every item is consumed.
-int copy_consume(rt_scene* s, const void* d_src, size_t n_items, size_t rec_bytes,
-                 const std::function<void(const unsigned char*, size_t, size_t)>& consume)
+// The host-buffer entry points' device -> host step.  queue_copy queues records [a, b) of d_src (after
+// the work already on the scene's stream) into the same offsets of pinned staging, in k chunks whose
+// arrivals are recorded by events; consume_copies then runs consume(stage, a, b) on the host pool
+// for each chunk's items as soon as that chunk has landed, so the host pass over one chunk overlaps
+// the DMA of the next (and whatever device work was queued after it).  Staging must be reserved
+// for every queued record first.
+struct CopyPlan {
+    size_t a[rt_scene::kCopyChunks], b[rt_scene::kCopyChunks];
+    int n = 0;
+};
+
+int queue_copy(rt_scene* s, CopyPlan& plan, const void* d_src, size_t a, size_t b, size_t rec_bytes, int k)
 {
-    const size_t bytes = n_items * rec_bytes;
-    HIP_TRY(s->stage.reserve(bytes));
-    const size_t K = std::max<size_t>(1, std::min<size_t>(rt_scene::kCopyChunks, bytes >> 20)); // >= 1 MB per chunk
-    const size_t per = (n_items + K - 1) / K;
-    for (size_t k = 0; k < K; k++) {
-        const size_t a = std::min(n_items, k * per), b = std::min(n_items, (k + 1) * per);
-        if (!s->copy_ev[k]) HIP_TRY(hipEventCreateWithFlags(&s->copy_ev[k], hipEventDisableTiming));
-        if (b > a)
-            HIP_TRY(hipMemcpyAsync(s->stage.p + a * rec_bytes, static_cast<const unsigned char*>(d_src) + a * rec_bytes,
-                                   (b - a) * rec_bytes, hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(hipEventRecord(s->copy_ev[k], s->stream));
+    k = std::max(1, std::min(k, rt_scene::kCopyChunks - plan.n));
+    const size_t per = (b - a + k - 1) / k;
+    for (int c = 0; c < k; c++) {
+        const size_t ca = std::min(b, a + c * per), cb = std::min(b, a + (c + 1) * per);
+        hipEvent_t& ev = s->copy_ev[plan.n];
+        if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        if (cb > ca)
+            HIP_TRY(hipMemcpyAsync(s->stage.p + ca * rec_bytes, static_cast<const unsigned char*>(d_src) + ca * rec_bytes,
+                                   (cb - ca) * rec_bytes, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipEventRecord(ev, s->stream));
+        plan.a[plan.n] = ca;
+        plan.b[plan.n] = cb;
+        plan.n++;
     }
-    // K chunks x S slices, handed out in order: the first tasks wait for the first chunk
+    return RT_OK;
+}
+
+int consume_copies(rt_scene* s, const CopyPlan& plan, const std::function<void(const unsigned char*, size_t, size_t)>& consume)
+{
+    // chunks x S slices, handed out in order: the first tasks wait for the first chunk
     const size_t S = (size_t)host_threads();
     std::atomic<int> failed{0};
-    host_run(K * S, [&](size_t t) {
+    host_run((size_t)plan.n * S, [&](size_t t) {
         const size_t k = t / S, j = t % S;
-        const size_t a0 = std::min(n_items, k * per), b0 = std::min(n_items, (k + 1) * per);
+        const size_t a0 = plan.a[k], b0 = plan.b[k];
         const size_t sl = (b0 - a0 + S - 1) / S;
         const size_t a = std::min(b0, a0 + j * sl), b = std::min(b0, a + sl);
         if (hipEventSynchronize(s->copy_ev[k]) != hipSuccess) {
@@ -1618,10 +1635,23 @@ int copy_consume(rt_scene* s, const void* d_src, size_t n_items, size_t rec_byte
         if (b > a) consume(s->stage.p, a, b);
     });
     if (failed) {
-        set_error("copy_consume: device -> host copy failed");
+        set_error("device -> host copy failed");
         return RT_ERR_HIP;
     }
     return RT_OK;
+}
+
+// n_items records of rec_bytes from d_src in up to kCopyChunks chunks of at least 1 MB.
+int copy_consume(rt_scene* s, const void* d_src, size_t n_items, size_t rec_bytes,
+                 const std::function<void(const unsigned char*, size_t, size_t)>& consume)
+{
+    const size_t bytes = n_items * rec_bytes;
+    HIP_TRY(s->stage.reserve(bytes));
+    CopyPlan plan;
+    const int K = (int)std::max<size_t>(1, std::min<size_t>(rt_scene::kCopyChunks, bytes >> 20));
+    int rc = queue_copy(s, plan, d_src, 0, n_items, rec_bytes, K);
+    if (rc != RT_OK) return rc;
+    return consume_copies(s, plan, consume);
 }
 
 } // namespace
@@ -2422,22 +2452,46 @@ int rt_render_tile(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, in
     HIP_TRY(s->sum.reserve(3 * npix));
     HIP_TRY(s->samples.reserve(npix));
     HIP_TRY(s->misses.reserve(npix));
+    HIP_TRY(s->colors.reserve(4 * npix)); // the caller's layout: one 32-B TileRec per pixel, x*h + y
+    HIP_TRY(s->stage.reserve(npix * sizeof(TileRec)));
+    HIP_TRY(s->rays_h.reserve(1));
     HIP_TRY(hipMemsetAsync(s->sum.p, 0, 3 * npix * sizeof(double), s->stream));
     HIP_TRY(hipMemsetAsync(s->samples.p, 0, npix * sizeof(uint32_t), s->stream));
     HIP_TRY(hipMemsetAsync(s->misses.p, 0, npix * sizeof(uint32_t), s->stream));
     HIP_TRY(hipMemsetAsync(s->rays.p, 0, sizeof(unsigned long long), s->stream));
-    rc = rt_render_device(s, x0, y0, w, h, spp, seed, sample_base, s->sum.p, s->samples.p, s->misses.p, s->rays.p,
-                          s->stream);
-    if (rc != RT_OK) return rc;
-    // the caller's layout on the device (one 32-B TileRec per pixel, x*h + y), copied in chunks into
-    // pinned staging and added into the caller's arrays chunk by chunk as the chunks land
-    // (copy_consume; a strided single-threaded transpose on the host took ~30 ms at 1080p)
-    HIP_TRY(s->colors.reserve(4 * npix)); // 32 B per pixel
-    HIP_TRY(s->rays_h.reserve(1));
     TileRec* d_rec = reinterpret_cast<TileRec*>(s->colors.p);
-    HIP_TRY(launch_tile_host_layout(w, h, s->sum.p, s->samples.p, s->misses.p, d_rec, s->stream));
-    HIP_TRY(hipMemcpyAsync(s->rays_h.p, s->rays.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
-    rc = copy_consume(s, d_rec, npix, sizeof(TileRec), [&](const unsigned char* st, size_t a, size_t b) {
+    // A large call renders in column bands, each a launch of its own whose records are copied and
+    // added into the caller's arrays (the band's columns are one contiguous range of x*h + y) while
+    // the next band renders: only the last band's copy and add are not hidden behind the kernel
+    // (1080p x 256 spp on bounce.txt: 8 ms of 27 ms per call in one launch).  Every band launch takes
+    // the whole tile's chunks per pixel, so the sums are those of one launch bit for bit.
+    // RTCORE_TILE_BANDS overrides the count (1 = one launch).
+    const double work = (double)npix * spp;
+    int nb = work >= 6.4e7 ? 4 : work >= 1.6e7 ? 2 : 1;
+    if (const char* e = getenv("RTCORE_TILE_BANDS")) nb = std::max(1, std::min(4, atoi(e)));
+    nb = std::max(1, std::min(nb, w / 64));
+    const int per_band_chunks = nb == 1 ? (int)std::max<size_t>(1, std::min<size_t>(rt_scene::kCopyChunks,
+                                                                                  (npix * sizeof(TileRec)) >> 20))
+                                        : rt_scene::kCopyChunks / nb;
+    CopyPlan plan;
+    for (int k = 0; k < nb; k++) {
+        const int a = nb == 1 ? 0 : (int)((int64_t)w * k / nb) & ~7, b = k + 1 == nb ? w : (int)((int64_t)w * (k + 1) / nb) & ~7;
+        const int wb = b - a;
+        const size_t off = (size_t)a * h;
+        PathParams p = make_params(s, x0 + a, y0, wb, h, spp, seed, sample_base, (double)npix);
+        rc = run_path(s, p, s->rays.p, s->stream);
+        if (rc != RT_OK) return rc;
+        HIP_TRY(launch_accumulate(p, s->sum.p + 3 * off, s->samples.p + off, s->misses.p + off, s->stream));
+        HIP_TRY(launch_tile_host_layout(wb, h, s->sum.p + 3 * off, s->samples.p + off, s->misses.p + off, d_rec + off,
+                                        s->stream));
+        if (k + 1 == nb)
+            HIP_TRY(hipMemcpyAsync(s->rays_h.p, s->rays.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
+        rc = queue_copy(s, plan, d_rec, off, off + (size_t)wb * h, sizeof(TileRec), per_band_chunks);
+        if (rc != RT_OK) return rc;
+    }
+    rc = end_op(s, s->stream);
+    if (rc != RT_OK) return rc;
+    rc = consume_copies(s, plan, [&](const unsigned char* st, size_t a, size_t b) {
         const TileRec* r = reinterpret_cast<const TileRec*>(st);
         for (size_t o = a; o < b; o++) {
             sum_rgb[o].r += r[o].r;
@@ -2448,7 +2502,7 @@ int rt_render_tile(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, in
         }
     });
     if (rc != RT_OK) return rc;
-    if (rays_out) *rays_out += s->rays_h.p[0]; // copied before the chunks, on the same stream
+    if (rays_out) *rays_out += s->rays_h.p[0]; // copied before the last band's chunks, on the same stream
     return RT_OK;
 }
 

@@ -118,21 +118,24 @@ def test_sample_level_agreement(rc, scenes):
     assert set(np.unique(g[np.all(g < 0, axis=-1)])) <= {-1.0}
 
 
-def test_host_tile_equals_device_render_1080p(rc, scenes):
-    """rt_render_tile (host arrays, SampleSet [x, y] order, added to) at the full 1080p frame equals
-    the device-resident render of the same samples, transposed, bit for bit; a second call adds."""
+@pytest.mark.parametrize("tile", [(0, 0, 1920, 1080, 4), (0, 0, 1920, 1080, 32), (3, 5, 1001, 777, 96)])
+def test_host_tile_equals_device_render_1080p(rc, scenes, tile):
+    """rt_render_tile (host arrays, SampleSet [x, y] order, added to) equals the device-resident
+    render of the same samples in one launch, transposed, bit for bit; a second call adds.  1080p at
+    4 spp is one launch; 1080p at 32 spp and a ragged 1001 x 777 tile at 96 spp render in 4 column
+    bands (band edges on multiples of 8 columns) whose copies overlap the next band's launch."""
     import torch
 
-    W, H, spp = 1920, 1080, 4
-    gpu = rc.GpuRaytracer(scenes["die.txt"], 0, size=(W, H))
+    x0, y0, W, H, spp = tile
+    gpu = rc.GpuRaytracer(scenes["die.txt"], 0, size=(1920, 1080))
     dev = torch.device("cuda", 0)
     d_sum = torch.zeros(3 * W * H, dtype=torch.float64, device=dev)
     d_n = torch.zeros(W * H, dtype=torch.int32, device=dev)
     d_m = torch.zeros(W * H, dtype=torch.int32, device=dev)
     d_r = torch.zeros(1, dtype=torch.int64, device=dev)
-    gpu.render_device(0, 0, W, H, spp, 5, 7, d_sum.data_ptr(), d_n.data_ptr(), d_m.data_ptr(), d_r.data_ptr(), 0)
+    gpu.render_device(x0, y0, W, H, spp, 5, 7, d_sum.data_ptr(), d_n.data_ptr(), d_m.data_ptr(), d_r.data_ptr(), 0)
     torch.cuda.synchronize(dev)
-    s, n, m, rays = gpu.render_tile(0, 0, W, H, spp, seed=5, sample_base=7)
+    s, n, m, rays = gpu.render_tile(x0, y0, W, H, spp, seed=5, sample_base=7)
     ds = d_sum.cpu().numpy().reshape(3, H, W).transpose(2, 1, 0)  # -> [x, y, rgb]
     assert np.array_equal(s, ds)
     assert np.array_equal(n, d_n.cpu().numpy().reshape(H, W).T.astype(np.uint32))
@@ -140,7 +143,7 @@ def test_host_tile_equals_device_render_1080p(rc, scenes):
     assert rays == int(d_r.item())
     lib, C_ = gpu.lib, __import__("ctypes")
     r2 = C_.c_uint64(0)
-    assert lib.rt_render_tile(gpu.handle, 0, 0, W, H, spp, 5, 7, s.ctypes.data_as(C_.POINTER(rc.rt_color)),
+    assert lib.rt_render_tile(gpu.handle, x0, y0, W, H, spp, 5, 7, s.ctypes.data_as(C_.POINTER(rc.rt_color)),
                               n.ctypes.data_as(C_.POINTER(C_.c_uint32)), m.ctypes.data_as(C_.POINTER(C_.c_uint32)),
                               C_.byref(r2)) == 0
     assert np.array_equal(s, 2 * ds) and np.all(n + m == 2 * spp) and r2.value == rays

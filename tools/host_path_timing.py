@@ -1,5 +1,6 @@
 """Rates through the host-buffer entry points (the PCIe-inclusive view; bench.py's `value` keeps the
-accumulators in HBM): rt_render_tile (spp samples per call into host SampleSet buffers) and
+accumulators in HBM): rt_render_tile (spp samples per call into host SampleSet buffers; column bands whose copies overlap
+the next band's launch, and one launch for comparison) and
 rt_render_tile_1spp (Raytracer.Render's one-pass contract, DoubleColor[w, h] per pass), 1080p
 bounce.txt camera 0.  Prints one JSON line.
 
@@ -21,16 +22,25 @@ scene = rc.SceneLoader.from_file(rc.scene_path("bounce.txt"))
 g = rc.GpuRaytracer(scene, 0, size=(W, H))
 out = {}
 for spp in (256, 16):
-    g.render_tile(0, 0, W, H, spp, seed=1)  # warm-up (buffers, specialised build)
-    t0 = time.perf_counter()
-    rays = 0
-    n = 5
-    for k in range(n):
-        s, ns, ms, r = g.render_tile(0, 0, W, H, spp, seed=1, sample_base=(k + 1) * spp)
-        rays += r
-    dt = (time.perf_counter() - t0) / n
-    out[f"render_tile_{spp}spp"] = {"ms_per_call": round(dt * 1e3, 2), "mrays_per_s": round(rays / n / dt / 1e6, 1),
-                                   "kernel_ms": round(g.last_kernel_ms(), 2)}
+    # column bands (the default for calls this large) against one launch (RTCORE_TILE_BANDS=1, read
+    # per call); kernel_ms is the one launch's path kernel
+    for bands in ("1", None):
+        if bands:
+            os.environ["RTCORE_TILE_BANDS"] = bands
+        else:
+            os.environ.pop("RTCORE_TILE_BANDS", None)
+        g.render_tile(0, 0, W, H, spp, seed=1)  # warm-up (buffers, specialised build)
+        t0 = time.perf_counter()
+        rays = 0
+        n = 5
+        for k in range(n):
+            s, ns, ms, r = g.render_tile(0, 0, W, H, spp, seed=1, sample_base=(k + 1) * spp)
+            rays += r
+        dt = (time.perf_counter() - t0) / n
+        rec = {"ms_per_call": round(dt * 1e3, 2), "mrays_per_s": round(rays / n / dt / 1e6, 1)}
+        if bands:
+            rec["kernel_ms"] = round(g.last_kernel_ms(), 2)
+        out[f"render_tile_{spp}spp" + ("_one_launch" if bands else "")] = rec
 buf = np.zeros((W, H, 3), np.float64)
 g.render_tile_1spp(0, 0, W, H, seed=1, sample_index=0, out=buf)
 for label, reuse in (("render_tile_1spp", True), ("render_tile_1spp_fresh", False)):
