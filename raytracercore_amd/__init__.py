@@ -370,11 +370,15 @@ class GpuRaytracer:
         _check(self.lib.rt_bvh_counts(self.handle, x0, y0, w, h, out.ctypes.data_as(C.POINTER(C.c_int32))))
         return out
 
-    def render_tile(self, x0: int, y0: int, w: int, h: int, spp: int, seed: int = 0, sample_base: int = 0):
-        """Accumulators (sum[w,h,3] f64, samples[w,h] u32, misses[w,h] u32, rays)."""
-        s = np.zeros((w, h, 3), np.float64)
-        n = np.zeros((w, h), np.uint32)
-        m = np.zeros((w, h), np.uint32)
+    def render_tile(self, x0: int, y0: int, w: int, h: int, spp: int, seed: int = 0, sample_base: int = 0, out=None):
+        """Accumulators (sum[w,h,3] f64, samples[w,h] u32, misses[w,h] u32, rays): new zeroed arrays, or
+        the caller's `out` = (sum, samples, misses), which the call adds into (SampleSet's merge)."""
+        if out is None:
+            out = (np.zeros((w, h, 3), np.float64), np.zeros((w, h), np.uint32), np.zeros((w, h), np.uint32))
+        s, n, m = out
+        for a, shape, dt in ((s, (w, h, 3), np.float64), (n, (w, h), np.uint32), (m, (w, h), np.uint32)):
+            if a.shape != shape or a.dtype != dt or not a.flags.c_contiguous:
+                raise ValueError("out must be C-contiguous (sum f64 [w, h, 3], samples u32 [w, h], misses u32 [w, h])")
         rays = C.c_uint64(0)
         _check(self.lib.rt_render_tile(self.handle, x0, y0, w, h, spp, seed, sample_base,
                                        s.ctypes.data_as(C.POINTER(rt_color)),
