@@ -207,6 +207,10 @@ struct rt_scene {
     HostBuf<unsigned long long> rays_h;
     static constexpr int kCopyChunks = 8; // chunked device -> host copies (copy_consume)
     std::array<hipEvent_t, kCopyChunks> copy_ev{};
+    // rt_render_tile: band k's records are copied on copy_stream once band_ev[k] (recorded on the
+    // scene's stream after the band's layout kernel) has fired, so band k + 1 renders meanwhile
+    hipStream_t copy_stream = nullptr;
+    std::array<hipEvent_t, kCopyChunks> band_ev{};
     DevBuf<uint32_t> samples, misses;
     DevBuf<int32_t> ids;
     bool stats_on = false;      // launch the instrumented kernel (rt_scene_set_stats)
@@ -250,6 +254,12 @@ struct rt_scene {
         if (done_ev) (void)hipEventDestroy(done_ev);
         for (hipEvent_t e : copy_ev)
             if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : band_ev)
+            if (e) (void)hipEventDestroy(e);
+        if (copy_stream) {
+            (void)hipStreamSynchronize(copy_stream);
+            (void)hipStreamDestroy(copy_stream);
+        }
         for (int i = 0; i < kTimeRing; i++) {
             if (t_start[i]) (void)hipEventDestroy(t_start[i]);
             if (t_end[i]) (void)hipEventDestroy(t_end[i]);
@@ -1599,7 +1609,8 @@ struct CopyPlan {
     int n = 0;
 };
 
-int queue_copy(rt_scene* s, CopyPlan& plan, const void* d_src, size_t a, size_t b, size_t rec_bytes, int k)
+int queue_copy(rt_scene* s, CopyPlan& plan, const void* d_src, size_t a, size_t b, size_t rec_bytes, int k,
+               hipStream_t stream)
 {
     k = std::max(1, std::min(k, rt_scene::kCopyChunks - plan.n));
     const size_t per = (b - a + k - 1) / k;
@@ -1609,8 +1620,8 @@ int queue_copy(rt_scene* s, CopyPlan& plan, const void* d_src, size_t a, size_t 
         if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         if (cb > ca)
             HIP_TRY(hipMemcpyAsync(s->stage.p + ca * rec_bytes, static_cast<const unsigned char*>(d_src) + ca * rec_bytes,
-                                   (cb - ca) * rec_bytes, hipMemcpyDeviceToHost, s->stream));
-        HIP_TRY(hipEventRecord(ev, s->stream));
+                                   (cb - ca) * rec_bytes, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipEventRecord(ev, stream));
         plan.a[plan.n] = ca;
         plan.b[plan.n] = cb;
         plan.n++;
@@ -1649,7 +1660,7 @@ int copy_consume(rt_scene* s, const void* d_src, size_t n_items, size_t rec_byte
     HIP_TRY(s->stage.reserve(bytes));
     CopyPlan plan;
     const int K = (int)std::max<size_t>(1, std::min<size_t>(rt_scene::kCopyChunks, bytes >> 20));
-    int rc = queue_copy(s, plan, d_src, 0, n_items, rec_bytes, K);
+    int rc = queue_copy(s, plan, d_src, 0, n_items, rec_bytes, K, s->stream);
     if (rc != RT_OK) return rc;
     return consume_copies(s, plan, consume);
 }
@@ -2460,16 +2471,19 @@ int rt_render_tile(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, in
     HIP_TRY(hipMemsetAsync(s->misses.p, 0, npix * sizeof(uint32_t), s->stream));
     HIP_TRY(hipMemsetAsync(s->rays.p, 0, sizeof(unsigned long long), s->stream));
     TileRec* d_rec = reinterpret_cast<TileRec*>(s->colors.p);
-    // A large call renders in column bands, each a launch of its own whose records are copied and
-    // added into the caller's arrays (the band's columns are one contiguous range of x*h + y) while
-    // the next band renders: only the last band's copy and add are not hidden behind the kernel
-    // (1080p x 256 spp on bounce.txt: 8 ms of 27 ms per call in one launch).  Every band launch takes
-    // the whole tile's chunks per pixel, so the sums are those of one launch bit for bit.
+    // A large call renders in column bands, each a launch of its own whose records are copied (on
+    // copy_stream) and added into the caller's arrays (the band's columns are one contiguous range
+    // of x*h + y) while the next band renders: only the last band's copy and add are not hidden
+    // behind the kernel.  Every band launch takes the whole tile's chunks per pixel, so the sums are
+    // those of one launch bit for bit.  bounce.txt 1080p, ms per call into the caller's arrays
+    // with 1 / 2 / 4 bands (tools/host_path_timing.py, profiles/r04/host_path_bands.log): 16 spp
+    // 4.17 / 3.89 / 3.54, 64 spp 8.13 / 7.88 / 7.21, 256 spp 22.05 / 20.95 / 20.86.
     // RTCORE_TILE_BANDS overrides the count (1 = one launch).
     const double work = (double)npix * spp;
-    int nb = work >= 6.4e7 ? 4 : work >= 1.6e7 ? 2 : 1;
+    int nb = work >= 1.6e7 ? 4 : work >= 4e6 ? 2 : 1;
     if (const char* e = getenv("RTCORE_TILE_BANDS")) nb = std::max(1, std::min(4, atoi(e)));
     nb = std::max(1, std::min(nb, w / 64));
+    if (!s->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&s->copy_stream, hipStreamNonBlocking));
     const int per_band_chunks = nb == 1 ? (int)std::max<size_t>(1, std::min<size_t>(rt_scene::kCopyChunks,
                                                                                   (npix * sizeof(TileRec)) >> 20))
                                         : rt_scene::kCopyChunks / nb;
@@ -2484,9 +2498,13 @@ int rt_render_tile(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, in
         HIP_TRY(launch_accumulate(p, s->sum.p + 3 * off, s->samples.p + off, s->misses.p + off, s->stream));
         HIP_TRY(launch_tile_host_layout(wb, h, s->sum.p + 3 * off, s->samples.p + off, s->misses.p + off, d_rec + off,
                                         s->stream));
-        if (k + 1 == nb)
-            HIP_TRY(hipMemcpyAsync(s->rays_h.p, s->rays.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
-        rc = queue_copy(s, plan, d_rec, off, off + (size_t)wb * h, sizeof(TileRec), per_band_chunks);
+        if (!s->band_ev[k]) HIP_TRY(hipEventCreateWithFlags(&s->band_ev[k], hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(s->band_ev[k], s->stream));
+        HIP_TRY(hipStreamWaitEvent(s->copy_stream, s->band_ev[k], 0));
+        if (k + 1 == nb) // (before the last chunks, so it has landed when they have)
+            HIP_TRY(hipMemcpyAsync(s->rays_h.p, s->rays.p, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                   s->copy_stream));
+        rc = queue_copy(s, plan, d_rec, off, off + (size_t)wb * h, sizeof(TileRec), per_band_chunks, s->copy_stream);
         if (rc != RT_OK) return rc;
     }
     rc = end_op(s, s->stream);
@@ -2502,7 +2520,7 @@ int rt_render_tile(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, in
         }
     });
     if (rc != RT_OK) return rc;
-    if (rays_out) *rays_out += s->rays_h.p[0]; // copied before the last band's chunks, on the same stream
+    if (rays_out) *rays_out += s->rays_h.p[0]; // copied before the last band's chunks, on the copy stream
     return RT_OK;
 }
 

@@ -118,12 +118,14 @@ def test_sample_level_agreement(rc, scenes):
     assert set(np.unique(g[np.all(g < 0, axis=-1)])) <= {-1.0}
 
 
-@pytest.mark.parametrize("tile", [(0, 0, 1920, 1080, 4), (0, 0, 1920, 1080, 32), (3, 5, 1001, 777, 96)])
+@pytest.mark.parametrize("tile", [(0, 0, 1920, 1080, 1), (0, 0, 1920, 1080, 4), (0, 0, 1920, 1080, 32),
+                                  (3, 5, 1001, 777, 96)])
 def test_host_tile_equals_device_render_1080p(rc, scenes, tile):
     """rt_render_tile (host arrays, SampleSet [x, y] order, added to) equals the device-resident
     render of the same samples in one launch, transposed, bit for bit; a second call adds.  1080p at
-    4 spp is one launch; 1080p at 32 spp and a ragged 1001 x 777 tile at 96 spp render in 4 column
-    bands (band edges on multiples of 8 columns) whose copies overlap the next band's launch."""
+    1 spp is one launch, at 4 spp 2 column bands; 1080p at 32 spp and a ragged 1001 x 777 tile at
+    96 spp render in 4 (band edges on multiples of 8 columns), each band's copy overlapping the next
+    band's launch."""
     import torch
 
     x0, y0, W, H, spp = tile

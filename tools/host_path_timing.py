@@ -21,10 +21,10 @@ W, H = 1920, 1080
 scene = rc.SceneLoader.from_file(rc.scene_path("bounce.txt"))
 g = rc.GpuRaytracer(scene, 0, size=(W, H))
 out = {}
-for spp in (256, 16):
-    # column bands (the default for calls this large) against one launch (RTCORE_TILE_BANDS=1, read
-    # per call); kernel_ms is the one launch's path kernel
-    for bands in ("1", None):
+BANDS = os.environ.get("HOST_TIMING_BANDS", "1").split(",")  # e.g. "1,2,4": band counts to compare
+for spp in (256, 64, 16):
+    # the default band count for the call against the forced counts (RTCORE_TILE_BANDS, read per call)
+    for bands in BANDS + [None]:
         if bands:
             os.environ["RTCORE_TILE_BANDS"] = bands
         else:
@@ -41,7 +41,7 @@ for spp in (256, 16):
             rays += r
         dt = (time.perf_counter() - t0) / n
         rec = {"ms_per_call": round(dt * 1e3, 2), "mrays_per_s": round(rays / n / dt / 1e6, 1)}
-        nb = 1 if bands else (4 if W * H * spp >= 6.4e7 else 2 if W * H * spp >= 1.6e7 else 1)
+        nb = int(bands) if bands else (4 if W * H * spp >= 1.6e7 else 2 if W * H * spp >= 4e6 else 1)
         rec["kernel_ms"] = round(float(np.sum(g.kernel_times(nb))), 2)  # the call's launches
         rec["launches"] = nb
         # a fresh set of arrays per call (np.zeros: pages mapped by the call's first touch)
@@ -49,7 +49,7 @@ for spp in (256, 16):
         for k in range(n):
             g.render_tile(0, 0, W, H, spp, seed=1, sample_base=(k + 1) * spp)
         rec["ms_per_call_fresh_arrays"] = round((time.perf_counter() - t0) / n * 1e3, 2)
-        out[f"render_tile_{spp}spp" + ("_one_launch" if bands else "")] = rec
+        out[f"render_tile_{spp}spp" + (f"_bands{bands}" if bands else "")] = rec
 buf = np.zeros((W, H, 3), np.float64)
 g.render_tile_1spp(0, 0, W, H, seed=1, sample_index=0, out=buf)
 for label, reuse in (("render_tile_1spp", True), ("render_tile_1spp_fresh", False)):
