@@ -327,7 +327,10 @@ __device__ __forceinline__ bool slab(float4 lo, float4 hi, V3 oi, V3 id, float t
 
 // Every primitive, group by group (GroupRec: x-rects | y-rects | z-rects | triangles | spheres).
 // The loop indices are wave-uniform, so the records arrive through scalar loads.  With CULL a
-// group is skipped when no lane of the wave meets its box before its current closest hit.
+// group is skipped when no lane of the wave meets its box before its current closest hit, and
+// with it the G.skip records that follow it (a super record: the box of a subtree of groups, no
+// primitives of its own).  The skip is a wave-uniform bound (skip_to), not a jump of the loop
+// index, so the scene-specialised build still unrolls the loop.
 // The record pointers are in the constant address space (RT_AS_CONST) or generic.
 // boxes: the frame array viewed as BoxRecs (they share it).
 template <bool CULL, bool STATS, class SceneT, class GroupP, class TestP, class RectP, class FrameP, class BoxP, class XfP>
@@ -338,15 +341,20 @@ __device__ __forceinline__ void trace_brute(const SceneT& s, GroupP groups, Test
     const V3 id = v3(slab_rcp_lean(d.x), slab_rcp_lean(d.y), slab_rcp_lean(d.z));
     const V3 oi = o * id;
     const int n_groups = CULL ? s.n_groups : 1; // the flat order is one group (1/d and o/d die after its rects)
+    int skip_to = 0;
 #ifdef RT_SCENE_CONST
 #pragma unroll // the scene-specialised build: every group's tests in line, their records literals
 #endif
     for (int g = 0; g < n_groups; g++) {
+        if (CULL && g < skip_to) continue;
         const GroupRec G = groups[g];
         if (CULL) {
-            if (STATS) n_node++; // the group's box: a node of a one-level tree (SURVEY 8(d) N_node)
+            if (STATS) n_node++; // the group's box: a node of a shallow tree (SURVEY 8(d) N_node)
             float tn;
-            if (!__any(slab<true>(G.lo, G.hi, oi, id, b.t, tn))) continue;
+            if (!__any(slab<true>(G.lo, G.hi, oi, id, b.t, tn))) {
+                skip_to = g + 1 + G.skip;
+                continue;
+            }
         }
         if (STATS) { // primitive tests actually made (groups the wave skipped are not counted)
             n_flat += G.n_rect[0] + G.n_rect[1] + G.n_rect[2] + G.n_flat_extra + (G.n_tri_sph & 0xFFFF);

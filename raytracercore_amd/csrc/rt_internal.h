@@ -152,7 +152,8 @@ struct alignas(16) GroupRec {
     int32_t frame_first;
     int16_t n_frames, n_boxes; // FrameRecs, then world BoxRecs, from frame_first
     int32_t n_flat_extra;      // faces tested through frames and boxes (statistics)
-    int32_t pad;
+    int32_t skip;              // super record (no primitives): the records after it that its box
+                               // holds, skipped with it; 0 for a group of primitives
 };
 
 // Intersection record of the fp32 kernel (64 B), one per primitive slot:

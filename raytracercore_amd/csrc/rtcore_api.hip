@@ -635,13 +635,24 @@ BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<
         }
     };
     const bool use_boxes = !getenv("RTCORE_NO_BOXES"); // A/B switch for measurements
-    auto build_order = [&](const std::vector<std::vector<int>>& groups) {
+    // skips[k] > 0: groups[k] lists a subtree's primitives for a super record (its box only) that
+    // holds the skips[k] records after it
+    auto build_order = [&](const std::vector<std::vector<int>>& groups, const std::vector<int>& skips) {
         BruteOrder o;
-        for (const auto& g : groups) {
+        for (size_t gi = 0; gi < groups.size(); gi++) {
+            const auto& g = groups[gi];
             GroupRec G;
             std::memset(&G, 0, sizeof G);
             float lo[3], hi[3];
             fbox(g, lo, hi);
+            if (skips[gi] > 0) {
+                G.lo = make_float4(lo[0], lo[1], lo[2], as_f((int)o.rects.size()));
+                G.hi = make_float4(hi[0], hi[1], hi[2], as_f((int)o.prims.size()));
+                G.frame_first = (int)o.frames.size();
+                G.skip = skips[gi];
+                o.groups.push_back(G);
+                continue;
+            }
             const int rect_first = (int)o.rects.size();
             int cnt[5] = {0, 0, 0, 0, 0};
             auto push_slot = [&](int i, PrimF f) {
@@ -773,7 +784,7 @@ BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<
     std::vector<int> all;
     for (int i = 0; i < n; i++)
         if (kind_of[i] != 5) all.push_back(i);
-    BruteOrder flat = build_order({all});
+    BruteOrder flat = build_order({all}, {0});
     int nr[3] = {flat.nr[0], flat.nr[1], flat.nr[2]}, nt = flat.nt, ns = flat.ns, np = 0;
     if (!flat.groups.empty()) {
         const GroupRec& G = flat.groups[0];
@@ -801,7 +812,50 @@ BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<
     int kGroupMax = jit_enabled() ? 8 : 4;
     if (const char* e = getenv("RTCORE_GROUP_MAX")) kGroupMax = std::max(1, atoi(e)); // tuning
     out.group_max = kGroupMax;
+    // Super records: a subtree (below the root) that the cut makes into at least kSuperMin groups
+    // also gets a record of its own box in front of them, so that a wave that misses it skips them
+    // all (die.txt: the die's five groups behind one box; background rays then test two boxes
+    // instead of six).  RTCORE_GROUP_SUPER sets kSuperMin (0: none).
+    int kSuperMin = 0; // (pending measurement)
+    if (const char* e = getenv("RTCORE_GROUP_SUPER")) kSuperMin = std::max(0, atoi(e));
     std::vector<std::vector<int>> cut;
+    std::vector<int> skips;
+    // Box-aware cut: the world rectangles that make closed boxes (the box finder on the whole
+    // scene) go to the first group that holds any of them, all together, so that the group's box
+    // finder makes them one slab test instead of rectangles spread over several groups (die.txt's
+    // cube: 4 + 1 + 1 faces in three groups).  RTCORE_GROUP_BOXES=0 turns it off.
+    bool group_boxes = false; // (pending measurement)
+    if (const char* e = getenv("RTCORE_GROUP_BOXES")) group_boxes = atoi(e) != 0;
+    std::vector<int> box_of(n, -1);
+    std::vector<std::vector<int>> box_faces;
+    if (group_boxes && use_boxes) {
+        std::vector<RectG> wr;
+        for (int i : all)
+            if (kind_of[i] < 3) wr.push_back(rect_geom(i, kind_of[i], nullptr, nullptr));
+        std::vector<char> used(wr.size(), 0);
+        for (const BoxFit& f6 : find_boxes(wr, used)) {
+            box_faces.emplace_back();
+            for (int j : f6.f)
+                if (j >= 0) {
+                    box_of[wr[j].i] = (int)box_faces.size() - 1;
+                    box_faces.back().push_back(wr[j].i);
+                }
+        }
+    }
+    std::vector<char> box_done(box_faces.size(), 0);
+    auto take_boxes = [&](const std::vector<int>& sub) { // a group's primitives, boxes whole
+        std::vector<int> g;
+        for (int i : sub) {
+            const int b = box_of[i];
+            if (b < 0) {
+                g.push_back(i);
+            } else if (!box_done[b]) {
+                box_done[b] = 1;
+                g.insert(g.end(), box_faces[b].begin(), box_faces[b].end());
+            }
+        }
+        return g;
+    };
     if ((int)all.size() <= 4096 && !sah.order.empty()) {
         std::function<void(int, std::vector<int>&)> leaves = [&](int ref, std::vector<int>& out) {
             if (ref < 0) {
@@ -815,22 +869,54 @@ BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<
             leaves(l, out);
             leaves(r, out);
         };
-        std::function<void(int)> split = [&](int ref) {
+        std::function<int(int)> n_cut = [&](int ref) { // groups the cut makes of a subtree
+            std::vector<int> sub;
+            leaves(ref, sub);
+            if ((int)sub.size() <= kGroupMax || ref < 0) return 1;
+            int l, r;
+            std::memcpy(&l, &sah.nodes[ref].lmin.w, 4);
+            std::memcpy(&r, &sah.nodes[ref].rmin.w, 4);
+            return n_cut(l) + n_cut(r);
+        };
+        std::function<void(int, bool)> split = [&](int ref, bool in_super) {
             std::vector<int> sub;
             leaves(ref, sub);
             if ((int)sub.size() <= kGroupMax || ref < 0) {
-                cut.push_back(sub);
+                std::vector<int> g = take_boxes(sub);
+                if (!g.empty()) {
+                    cut.push_back(std::move(g));
+                    skips.push_back(0);
+                }
                 return;
             }
             int l, r;
             std::memcpy(&l, &sah.nodes[ref].lmin.w, 4);
             std::memcpy(&r, &sah.nodes[ref].rmin.w, 4);
-            split(l);
-            split(r);
+            const size_t at = cut.size();
+            // one level: a super record inside another mostly repeats its box (die.txt: the die
+            // and the die minus a face's pips)
+            const bool super = kSuperMin > 0 && !in_super && ref != sah.root && n_cut(ref) >= kSuperMin;
+            if (super) {
+                cut.push_back(sub);
+                skips.push_back(0);
+            }
+            split(l, in_super || super);
+            split(r, in_super || super);
+            if (super) {
+                skips[at] = (int)(cut.size() - at - 1);
+                // its box: the primitives of the groups it holds (a box taken whole may reach
+                // outside the subtree); a super record holding fewer than two groups is dropped
+                cut[at].clear();
+                for (size_t k = at + 1; k < cut.size(); k++) cut[at].insert(cut[at].end(), cut[k].begin(), cut[k].end());
+                if (skips[at] < 2) {
+                    cut.erase(cut.begin() + (long)at);
+                    skips.erase(skips.begin() + (long)at);
+                }
+            }
         };
-        split(sah.root);
+        split(sah.root, false);
     }
-    BruteOrder grouped = cut.empty() ? BruteOrder{} : build_order(cut);
+    BruteOrder grouped = cut.empty() ? BruteOrder{} : build_order(cut, skips);
     out.flat = std::move(flat);
     out.grouped = std::move(grouped);
     for (int k = 0; k < 3; k++) out.nr[k] = nr[k];
@@ -883,8 +969,10 @@ MatTable make_materials(const std::vector<HostPrim>& H, double air_ior)
     return t;
 }
 
-// The grouped order's groups sorted by the distance from the camera to their boxes (stable).
-std::vector<GroupRec> groups_nearest_first(std::vector<GroupRec> g, const CameraD& cam)
+// The grouped order's records sorted by the distance from the camera to their boxes (stable), as
+// a tree: a super record keeps the records it holds (its skip) right behind it, sorted among
+// themselves the same way.
+std::vector<GroupRec> groups_nearest_first(const std::vector<GroupRec>& g, const CameraD& cam)
 {
     const double px = cam.position.x, py = cam.position.y, pz = cam.position.z;
     auto dist2 = [&](const GroupRec& G) {
@@ -894,8 +982,19 @@ std::vector<GroupRec> groups_nearest_first(std::vector<GroupRec> g, const Camera
         const double dz = std::max({0.0, (double)G.lo.z - pz, pz - (double)G.hi.z});
         return dx * dx + dy * dy + dz * dz;
     };
-    std::stable_sort(g.begin(), g.end(), [&](const GroupRec& a, const GroupRec& b) { return dist2(a) < dist2(b); });
-    return g;
+    std::vector<GroupRec> out;
+    std::function<void(size_t, size_t)> emit = [&](size_t a, size_t b) { // the sibling subtrees in [a, b)
+        std::vector<std::pair<size_t, size_t>> sib;
+        for (size_t i = a; i < b; i += 1 + (size_t)std::max(0, g[i].skip))
+            sib.push_back({i, std::min(b, i + 1 + (size_t)std::max(0, g[i].skip))});
+        std::stable_sort(sib.begin(), sib.end(), [&](const auto& x, const auto& y) { return dist2(g[x.first]) < dist2(g[y.first]); });
+        for (const auto& [i, e] : sib) {
+            out.push_back(g[i]);
+            emit(i + 1, e);
+        }
+    };
+    emit(0, g.size());
+    return out;
 }
 
 // The fp32 transform rows of a transformed sphere (XformF).
@@ -1313,7 +1412,7 @@ int calibrate_grouping(rt_scene* s)
     if (rays == 0) return RT_OK;
     // relative costs of a rect/triangle test, a sphere test and a group box test (instruction counts)
     const double flat = 20.0 * (n_bvh - s->dev.n_sph) + 30.0 * s->dev.n_sph;
-    const double grouped = 15.0 * s->dev.n_groups_gr + (20.0 * st[1] + 30.0 * st[2]) / (double)rays;
+    const double grouped = (15.0 * st[0] + 20.0 * st[1] + 30.0 * st[2]) / (double)rays; // st[0]: box tests made
     s->grouped_measured = flat / std::max(grouped, 1e-9);
     return resolve_traversal(s);
 }

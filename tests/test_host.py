@@ -271,6 +271,52 @@ def test_scene_specialised_header_of_shipped_scenes(rc, name, grouped, tmp_path)
     assert "rt_path_const" in (tmp_path / "k.s").read_text()
 
 
+def _group_records(h):
+    import re
+    import struct
+
+    w = [int(x, 16) for x in re.search(r"kGroupsW\[\d+\][^{]*\{([^}]*)\}", h).group(1).split(",")]
+    recs = []
+    for k in range(0, len(w), 16):
+        r = w[k:k + 16]
+        f = [struct.unpack("f", struct.pack("I", v))[0] for v in r[:8]]
+        recs.append({"lo": f[0:3], "hi": f[4:7], "n_rect": sum(r[8:11]), "n_tri": r[11] & 0xFFFF,
+                     "n_sph": r[11] >> 16, "n_frames": r[13] & 0xFFFF, "n_boxes": r[13] >> 16,
+                     "extra": r[14], "skip": r[15]})
+    return recs
+
+
+@pytest.mark.parametrize("name", ["die.txt", "bounce.txt"])
+def test_grouped_order_records(rc, name):
+    """The grouped order's records, as the scene-specialised header carries them for each camera:
+    super records (a box, no primitives, skip > 0) hold the records right behind them, are not
+    nested, and their box contains every record they hold; the groups together test every
+    non-plane primitive once (the flat order's count); the closed boxes of the scene are whole
+    groups' boxes (box-aware cut), so die.txt's cube is one box test."""
+    scene = rc.SceneLoader.from_file(rc.scene_path(name))
+    flat = _group_records(rc.jit_header(scene, 0, size=(1920, 1080), grouped=False))
+    assert len(flat) == 1 and flat[0]["skip"] == 0
+    total = lambda g: g["n_rect"] + g["n_tri"] + g["n_sph"] + g["extra"]
+    for cam in range(3 if name == "die.txt" else 1):
+        recs = _group_records(rc.jit_header(scene, cam, size=(1920, 1080), grouped=True))
+        i = 0
+        while i < len(recs):
+            g = recs[i]
+            if g["skip"] > 0:
+                assert total(g) == 0 and g["n_frames"] == 0 and g["n_boxes"] == 0
+                held = recs[i + 1:i + 1 + g["skip"]]
+                assert len(held) == g["skip"] >= 2
+                for c in held:
+                    assert c["skip"] == 0  # one level
+                    assert all(g["lo"][k] <= c["lo"][k] and c["hi"][k] <= g["hi"][k] for k in range(3))
+            i += 1
+        assert sum(total(g) for g in recs if g["skip"] == 0) == total(flat[0])
+        if name == "die.txt" and os.environ.get("RTCORE_GROUP_BOXES", "0") != "0":
+            assert sum(g["n_boxes"] for g in recs) == 1 and sum(g["n_rect"] for g in recs) == 0
+        if name == "die.txt" and os.environ.get("RTCORE_GROUP_SUPER", "0") != "0":
+            assert sum(g["skip"] > 0 for g in recs) == 1
+
+
 def test_experiment_patches_apply():
     """Cost experiments live in tools/exp_patch.py, not in the product kernel: every patch's anchors
     occur exactly once in kernels_path.hip, and the kernel holds no experiment switches."""
