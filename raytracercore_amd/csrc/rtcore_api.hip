@@ -815,16 +815,20 @@ BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<
     // Super records: a subtree (below the root) that the cut makes into at least kSuperMin groups
     // also gets a record of its own box in front of them, so that a wave that misses it skips them
     // all (die.txt: the die's five groups behind one box; background rays then test two boxes
-    // instead of six).  RTCORE_GROUP_SUPER sets kSuperMin (0: none).
-    int kSuperMin = 0; // (pending measurement)
+    // instead of six: 6.0 -> 4.69 box tests per ray, C3 26.81 -> 25.64 ms in the same call,
+    // profiles/r04/ab_group_super_boxes.log).  RTCORE_GROUP_SUPER sets kSuperMin (0: none).
+    int kSuperMin = 3;
     if (const char* e = getenv("RTCORE_GROUP_SUPER")) kSuperMin = std::max(0, atoi(e));
     std::vector<std::vector<int>> cut;
     std::vector<int> skips;
-    // Box-aware cut: the world rectangles that make closed boxes (the box finder on the whole
-    // scene) go to the first group that holds any of them, all together, so that the group's box
-    // finder makes them one slab test instead of rectangles spread over several groups (die.txt's
-    // cube: 4 + 1 + 1 faces in three groups).  RTCORE_GROUP_BOXES=0 turns it off.
-    bool group_boxes = false; // (pending measurement)
+    // Box-aware cut (RTCORE_GROUP_BOXES=1, off): the world rectangles that make closed boxes (the
+    // box finder on the whole scene) go to the first group that holds any of them, all together,
+    // so that the group's box finder makes them one slab test instead of rectangles spread over
+    // several groups (die.txt's cube: 4 + 1 + 1 faces in three groups).  Measured slower on
+    // die.txt (C3 26.81 -> 28.73 ms; with super records 25.64 -> 27.56): the group that takes
+    // the cube spans the whole die, so nearly every ray that meets the die tests its pips too
+    // (sphere tests per ray 4.61 -> 6.18).
+    bool group_boxes = false;
     if (const char* e = getenv("RTCORE_GROUP_BOXES")) group_boxes = atoi(e) != 0;
     std::vector<int> box_of(n, -1);
     std::vector<std::vector<int>> box_faces;

@@ -313,7 +313,7 @@ def test_grouped_order_records(rc, name):
         assert sum(total(g) for g in recs if g["skip"] == 0) == total(flat[0])
         if name == "die.txt" and os.environ.get("RTCORE_GROUP_BOXES", "0") != "0":
             assert sum(g["n_boxes"] for g in recs) == 1 and sum(g["n_rect"] for g in recs) == 0
-        if name == "die.txt" and os.environ.get("RTCORE_GROUP_SUPER", "0") != "0":
+        if name == "die.txt" and os.environ.get("RTCORE_GROUP_SUPER", "3") != "0":
             assert sum(g["skip"] > 0 for g in recs) == 1
 
 

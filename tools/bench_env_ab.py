@@ -2,7 +2,7 @@
 process never touches the GPU), in the order given, so that run-to-run drift shows up as a
 difference between the repeats of one setting.
 usage: tools/bench_env_ab.py "VAR=a" "VAR=b" "" "VAR=a" -- [bench.py args]
-("" = the default environment).  Prints one line per run: setting, ms_per_step, kernel_ms."""
+("" = the default environment).  Prints one line per run: setting, ms_per_step, kernel_ms and the instrumented launch's tests per ray."""
 import json
 import os
 import subprocess
@@ -26,7 +26,9 @@ def main():
             print(f"{setting or 'default'}: failed rc={r.returncode}\n{r.stderr[-2000:]}", flush=True)
             sys.exit(1)
         d = json.loads(lines[-1])
-        print(f"{setting or 'default':32s} ms_per_step {d['ms_per_step']:.3f} kernel_ms {d['kernel_ms']:.3f}", flush=True)
+        per_ray = (d.get("path_stats") or {}).get("per_ray", {})
+        print(f"{setting or 'default':32s} ms_per_step {d['ms_per_step']:.3f} kernel_ms {d['kernel_ms']:.3f} "
+              f"per_ray {json.dumps(per_ray)}", flush=True)
 
 
 if __name__ == "__main__":
