@@ -1,7 +1,7 @@
 """A/B of bench.py under environment settings, each setting a child process of its own (this
 process never touches the GPU), in the order given, so that run-to-run drift shows up as a
 difference between the repeats of one setting.
-usage: tools/bench_env_ab.py "VAR=a" "VAR=b" "" "VAR=a" -- [bench.py args]
+usage: tools/bench_env_ab.py "VAR=a" "VAR=b;OTHER=c d" "" "VAR=a" -- [bench.py args]
 ("" = the default environment).  Prints one line per run: setting, ms_per_step, kernel_ms and the instrumented launch's tests per ray."""
 import json
 import os
@@ -16,9 +16,10 @@ def main():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for setting in settings:
         env = dict(os.environ)
-        for kv in setting.split():
-            k, v = kv.split("=", 1)
-            env[k] = v
+        for kv in setting.split(";"):  # "A=1;B=x y": variables separated by ';' (values may hold spaces)
+            if kv.strip():
+                k, v = kv.strip().split("=", 1)
+                env[k] = v
         r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--no-cpu-baseline"] + bench_args,
                            env=env, capture_output=True, text=True, timeout=600)
         lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
