@@ -282,3 +282,42 @@ def test_c1_bounce256_against_oracle(rc, scenes):
                                                                             threads=min(16, os.cpu_count() or 1))
     _assert_parity(g, (so, no, mo, rays_o), spp, label="C1")
     gpu.close()
+
+
+def _cluster_scene_text():
+    """Three clusters of small spheres and a small box in a closed room, lit by one emissive sphere:
+    the grouped order puts groups of the clusters behind a super record."""
+    lines = ["size 96 64", "camera 0 -7 2.5, 0 0 0.5, 0 0 1, 65", "ambient color .05 .05 .05",
+             "emission 6 6 6", "sphere 0 0 4.2 .5", "emission 0 0 0",
+             "twosided false", "invert true", "diffuse .7 .7 .7", "specular .1 .1 .1", "cube 0 0 1.5 12 12 6 all",
+             "invert false", "twosided true", "shininess 40"]
+    centres = [(-2.5, 0.5, 0.2), (2.3, -0.4, 0.6), (0.0, 2.0, 1.4)]
+    for c, (cx, cy, cz) in enumerate(centres):
+        lines.append(f"diffuse {0.3 + 0.2 * c:.2f} .5 {0.8 - 0.2 * c:.2f}")
+        lines.append(f"specular .2 .2 .2")
+        for k in range(11):
+            dx, dy, dz = 0.42 * (k % 3) - 0.42, 0.42 * ((k // 3) % 2) - 0.21, 0.42 * (k // 6) - 0.21
+            lines.append(f"sphere {cx + dx:.3f} {cy + dy:.3f} {cz + dz:.3f} .17")
+    lines += ["diffuse .9 .8 .2", "cube 0.3 -1.5 -0.6 .8 .8 .8 all"]
+    return "\n".join(lines) + "\n"
+
+
+@pytest.mark.parametrize("mode", ["GROUPED", "BRUTE"])
+def test_sphere_clusters_against_oracle(rc, mode):
+    """Grouped order with super records (one per sphere cluster) and the wave-uniform sphere and box
+    skips, against the oracle and the brute-force order: IDs exact, accumulators within the parity
+    bound."""
+    scene = rc.SceneLoader.from_text(_cluster_scene_text())
+    size = (96, 64)
+    h = rc.jit_header(scene, 0, size=size, grouped=True)
+    import re
+    w = [int(x, 16) for x in re.search(r"kGroupsW\[\d+\][^{]*\{([^}]*)\}", h).group(1).split(",")]
+    skips = [w[k + 15] for k in range(0, len(w), 16)]
+    assert sum(1 for v in skips if v > 0) >= 1, skips  # a super record in the grouped order
+    gpu = rc.GpuRaytracer(scene, 0, size=size, traversal=getattr(rc, "RT_TRAVERSAL_" + mode))
+    orc = _oracle(rc, scene, size)
+    assert np.array_equal(gpu.primary_ids(), orc.primary_ids())
+    spp = 64
+    _assert_parity(gpu.render_tile(0, 0, *size, spp, seed=12), orc.render_tile(0, 0, *size, spp, seed=12), spp,
+                   label=f"sphere clusters {mode}")
+    gpu.close()
