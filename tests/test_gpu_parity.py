@@ -152,12 +152,12 @@ def test_host_tile_equals_device_render_1080p(rc, scenes, tile):
     gpu.close()
 
 
-@pytest.mark.parametrize("tile", [(0, 0, 1920, 1080), (3, 5, 1001, 777)])
+@pytest.mark.parametrize("tile", [(0, 0, 1920, 1080), (3, 5, 1001, 777), (3, 5, 1601, 777)])
 def test_one_pass_equals_device_render(rc, scenes, tile):
     """rt_render_tile_1spp (Raytracer.Render's one pass, copied in chunks as fp32 and widened on the
     host) equals the device-resident 1-spp render of the same sample: the colour where the sample
-    hit, Placeholder (-1) where it missed, bit for bit; a whole 1080p frame and a ragged tile whose
-    pixel count splits unevenly over the copy chunks."""
+    hit, Placeholder (-1) where it missed, bit for bit; a whole 1080p frame and ragged tiles whose
+    pixel counts split unevenly over the copy chunks."""
     import torch
 
     x0, y0, w, h = tile
