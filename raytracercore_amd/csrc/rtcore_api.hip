@@ -2580,10 +2580,13 @@ int rt_render_tile(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, in
     // behind the kernel.  Every band launch takes the whole tile's chunks per pixel, so the sums are
     // those of one launch bit for bit.  bounce.txt 1080p, ms per call into the caller's arrays
     // with 1 / 2 / 4 bands (tools/host_path_timing.py, profiles/r04/host_path_bands.log): 16 spp
-    // 4.17 / 3.89 / 3.54, 64 spp 8.13 / 7.88 / 7.21, 256 spp 22.05 / 20.95 / 20.86.
+    // 4.17 / 3.89 / 3.54, 64 spp 8.13 / 7.88 / 7.21, 256 spp 22.05 / 20.95 / 20.86; after the
+    // round's kernel gains (profiles/r04/host_path_timing.log, 1 / 4 bands) 16 spp 4.33 / 4.00, 64 spp
+    // 7.99 / 7.49, 256 spp 19.86 / 20.04: a long call gains less from the overlap than its band
+    // launches' tails cost, so from 2.5e8 samples per call it is one launch again.
     // RTCORE_TILE_BANDS overrides the count (1 = one launch).
     const double work = (double)npix * spp;
-    int nb = work >= 1.6e7 ? 4 : work >= 4e6 ? 2 : 1;
+    int nb = work >= 2.5e8 ? 1 : work >= 1.6e7 ? 4 : work >= 4e6 ? 2 : 1;
     if (const char* e = getenv("RTCORE_TILE_BANDS")) nb = std::max(1, std::min(4, atoi(e)));
     nb = std::max(1, std::min(nb, w / 64));
     if (!s->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&s->copy_stream, hipStreamNonBlocking));

@@ -125,7 +125,7 @@ def test_host_tile_equals_device_render_1080p(rc, scenes, tile):
     render of the same samples in one launch, transposed, bit for bit; a second call adds.  1080p at
     1 spp is one launch, at 4 spp 2 column bands; 1080p at 32 spp and a ragged 1001 x 777 tile at
     96 spp render in 4 (band edges on multiples of 8 columns), each band's copy overlapping the next
-    band's launch."""
+    band's launch (calls of 2.5e8 samples and more are one launch again)."""
     import torch
 
     x0, y0, W, H, spp = tile

@@ -41,7 +41,7 @@ for spp in (256, 64, 16):
             rays += r
         dt = (time.perf_counter() - t0) / n
         rec = {"ms_per_call": round(dt * 1e3, 2), "mrays_per_s": round(rays / n / dt / 1e6, 1)}
-        nb = int(bands) if bands else (4 if W * H * spp >= 1.6e7 else 2 if W * H * spp >= 4e6 else 1)
+        nb = int(bands) if bands else (1 if W * H * spp >= 2.5e8 else 4 if W * H * spp >= 1.6e7 else 2 if W * H * spp >= 4e6 else 1)
         rec["kernel_ms"] = round(float(np.sum(g.kernel_times(nb))), 2)  # the call's launches
         rec["launches"] = nb
         # a fresh set of arrays per call (np.zeros: pages mapped by the call's first touch)
