@@ -1464,7 +1464,10 @@ __global__ void __launch_bounds__(256, WIDTH == 4 ? RT_BVH_WAVES : RT_BVH2_WAVES
         // p.spec lanes are blocked (a second leaf reached, or no node left) or no lane can visit a
         // node, so an iteration is one kind of step instead of both.  Node culling uses the best hit
         // so far (the pending leaf not yet tested): more visits, the same closest hit.
-        const bool can_node = trav && more && ref >= 0;
+#ifndef RT_SPEC_RUNAHEAD
+#define RT_SPEC_RUNAHEAD 1 // 0: a lane with a pending leaf waits for the leaf step instead of visiting on
+#endif
+        const bool can_node = trav && more && ref >= 0 && (RT_SPEC_RUNAHEAD || pend < 0);
         const bool blocked = trav && pend >= 0 && !can_node;
         const bool leaf_step = __ballot(can_node) == 0 || __popcll(__ballot(blocked)) >= p.spec; // wave-uniform
         if (STATS) { // lane slots of this iteration (the BVH kernels reuse the brute-force cycle counters):
