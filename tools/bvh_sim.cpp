@@ -11,7 +11,7 @@
 // Boxes are the exact fp32 child boxes (no quantisation) in all three, so the figures compare the
 // tree shapes and orders only.  Primitives are tested in fp64 (Moller-Trumbore, Mirror
 // parallelograms), spheres by the quadratic.
-// build: make -C raytracercore_amd/csrc bvh_sim;  run: raytracercore_amd/csrc/_obj/bvh_sim SCENE [W H step]
+// build: make -C raytracercore_amd/csrc bvh_sim;  run: raytracercore_amd/csrc/_obj/bvh_sim SCENE [W H step [spec_frac [bounces]]]
 #include <algorithm>
 #include <array>
 #include <cmath>
@@ -230,7 +230,7 @@ int trace(const Wide& W, const SahBvh& b2, const std::vector<HostPrim>& H, const
 int main(int argc, char** argv)
 {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: bvh_sim SCENE [W H step]\n");
+        std::fprintf(stderr, "usage: bvh_sim SCENE [W H step [spec_frac [bounces]]]\n");
         return 2;
     }
     std::ifstream f(argv[1]);
@@ -244,6 +244,10 @@ int main(int argc, char** argv)
     }
     const int W = argc > 3 ? atoi(argv[2]) : 1920, Hh = argc > 3 ? atoi(argv[3]) : 1080;
     const int step = argc > 4 ? atoi(argv[4]) : 8;
+    // optional: the fraction of bounces that reflect as a mirror instead of diffusely, and the
+    // number of bounces after the camera ray (defaults 0 and 2: camera rays and two diffuse bounces)
+    const double spec_frac = argc > 5 ? atof(argv[5]) : 0.0;
+    const int n_bounces = argc > 6 ? atoi(argv[6]) : 2;
     const std::vector<HostPrim> H = prepare_prims(ps.prims.data(), (int)ps.prims.size());
     const SahBvh b2 = build_sah_bvh(H, H.size() > 256 ? 3 : 2);
     Wide w4, w8s, w8o;
@@ -273,7 +277,7 @@ int main(int argc, char** argv)
             r.o[0] = cd.position.x;
             r.o[1] = cd.position.y;
             r.o[2] = cd.position.z;
-            for (int bounce = 0; bounce < 3; bounce++) {
+            for (int bounce = 0; bounce <= n_bounces; bounce++) {
                 double t4, t8, t8o;
                 const int h4 = trace(w4, b2, H, r, 0, t4, s4);
                 trace(w8s, b2, H, r, 0, t8, s8s);
@@ -297,6 +301,14 @@ int main(int argc, char** argv)
                     for (int a = 0; a < 3; a++) n[a] = -n[a];
                 double p0[3];
                 for (int a = 0; a < 3; a++) p0[a] = r.o[a] + t4 * r.d[a] + 1e-6 * n[a];
+                if (spec_frac > 0 && U(rng) < spec_frac) { // mirror reflection about n
+                    const double dn = r.d[0] * n[0] + r.d[1] * n[1] + r.d[2] * n[2];
+                    for (int a = 0; a < 3; a++) {
+                        r.o[a] = p0[a];
+                        r.d[a] -= 2 * dn * n[a];
+                    }
+                    continue;
+                }
                 // cosine-weighted direction about n
                 const double u1 = U(rng), u2 = U(rng), rr = std::sqrt(u1), ph = 2 * M_PI * u2;
                 double tx[3] = {std::fabs(n[0]) < 0.9 ? 1.0 : 0.0, std::fabs(n[0]) < 0.9 ? 0.0 : 1.0, 0};
