@@ -33,8 +33,54 @@ struct Sampler {
     double next() { return rt_rng_next_double(&rng); }
 };
 
+// System.Random of .NET Core 3.1 (the BCL the reference targets, RaytracerCore.csproj:5; not
+// vendored): Knuth's subtractive generator as the BCL implements it, including its second
+// index starting at 21 (so X[n] = X[n-55] - X[n-34] mod int.MaxValue), NextDouble =
+// InternalSample() / int.MaxValue.  Diagnostic only: the shared counter-based stream
+// (include/rtcore_rng.h) is the normative one; this one lets the oracle draw the way one
+// reference worker thread does (Raytracer.cs:48, one Random per worker, consumed in pixel order).
+struct NetRandom {
+    int32_t seed_array[56];
+    int inext = 0, inextp = 21;
+    explicit NetRandom(int32_t seed)
+    {
+        const int32_t MBIG = 0x7fffffff, MSEED = 161803398;
+        int32_t subtraction = (seed == INT32_MIN) ? MBIG : (seed < 0 ? -seed : seed);
+        int32_t mj = MSEED - subtraction, mk = 1;
+        std::memset(seed_array, 0, sizeof(seed_array));
+        seed_array[55] = mj;
+        int ii = 0;
+        for (int i = 1; i < 55; i++) {
+            if ((ii += 21) >= 55) ii -= 55;
+            seed_array[ii] = mk;
+            mk = mj - mk;
+            if (mk < 0) mk += MBIG;
+            mj = seed_array[ii];
+        }
+        for (int k = 1; k < 5; k++)
+            for (int i = 1; i < 56; i++) {
+                int n = i + 30;
+                if (n >= 55) n -= 55;
+                seed_array[i] -= seed_array[1 + n];
+                if (seed_array[i] < 0) seed_array[i] += MBIG;
+            }
+    }
+    double next()
+    {
+        const int32_t MBIG = 0x7fffffff;
+        if (++inext >= 56) inext = 1;
+        if (++inextp >= 56) inextp = 1;
+        int32_t r = seed_array[inext] - seed_array[inextp];
+        if (r == MBIG) r--;
+        if (r < 0) r += MBIG;
+        seed_array[inext] = r;
+        return r * (1.0 / MBIG);
+    }
+};
+
 // Raytracer.RandomShine (Raytracer.cs:51-56).
-V4 random_shine(Sampler& rs, V4 dir, double shininess)
+template <class S>
+V4 random_shine(S& rs, V4 dir, double shininess)
 {
     double z = shininess == kInf ? 1 : std::pow(rs.next(), 1 / shininess);
     double theta = rs.next() * kPi * 2;
@@ -43,8 +89,11 @@ V4 random_shine(Sampler& rs, V4 dir, double shininess)
 
 // Raytracer.GetColor(Ray, ref DebugRay[]) (Raytracer.cs:65-246).  Returns the colour;
 // `rays` counts Scene.RayTrace calls.
-Col get_color(const Scene& sc, Ray ray, Sampler& rs, int& rays, std::vector<Leaf>& scratch)
+template <class S>
+Col get_color(const Scene& sc, Ray ray, S& rs, int& rays, std::vector<Leaf>& scratch, int32_t* trace = nullptr)
 {
+    // trace (diagnostic, may be null): per bounce i, trace[2i] = primitive hit (-1 miss),
+    // trace[2i+1] = event (1 diffuse, 2 specular, 3 specular fail, 4 transmitted, 5 emission, 0 other)
     Hit prev, hit;
     bool have_prev = false;
     Col tint = col(1);
@@ -52,6 +101,7 @@ Col get_color(const Scene& sc, Ray ray, Sampler& rs, int& rays, std::vector<Leaf
         if (i % 3 == 0) ray = ray_directional(ray.o, ray.d);
         hit = sc.raytrace(ray, have_prev ? &prev : nullptr, scratch);
         rays++;
+        if (trace) trace[2 * i] = hit.prim;
         if (hit.prim < 0) {
             if (i == 0) return col(-1);
             return sc.ambient;
@@ -100,12 +150,16 @@ Col get_color(const Scene& sc, Ray ray, Sampler& rs, int& rays, std::vector<Leaf
             have_out = true;
             new_tint = pr.refraction();
             if (hit.inside) new_tint = col(1);
+            if (trace) trace[2 * i + 1] = 4;
         } else if (spec_lum != 0 && (ray_rand -= spec_lum) <= 0) {
             V4 od = ray.d + (rough * (cs * 2)); // Raytracer.Reflection (:58-61)
             if (dot(od, hit.normal) > 0) {
                 out = Ray{hit.pos, od};
                 have_out = true;
                 new_tint = pr.specular();
+                if (trace) trace[2 * i + 1] = 2;
+            } else if (trace) {
+                trace[2 * i + 1] = 3;
             }
         } else if (diff_lum != 0 && (ray_rand -= diff_lum) <= 0) {
             double z = (2 * std::acos(rs.next())) / kPi;
@@ -113,7 +167,9 @@ Col get_color(const Scene& sc, Ray ray, Sampler& rs, int& rays, std::vector<Leaf
             out = Ray{hit.pos, create_horizon(hit.normal, z, theta)};
             have_out = true;
             new_tint = pr.diffuse;
+            if (trace) trace[2 * i + 1] = 1;
         } else {
+            if (trace) trace[2 * i + 1] = 5;
             break; // emission
         }
         // `outRay == Ray.Zero` (Raytracer.cs:231): origin and direction both zero (XYZ)
@@ -128,7 +184,8 @@ Col get_color(const Scene& sc, Ray ray, Sampler& rs, int& rays, std::vector<Leaf
 }
 
 // Raytracer.GetCameraRay (Raytracer.cs:262-282).
-Ray camera_ray(const Camera& cam, Sampler& rs, int x, int y)
+template <class S>
+Ray camera_ray(const Camera& cam, S& rs, int x, int y)
 {
     double dof = cam.dof_amount;
     double sx = x + rs.next();
@@ -488,6 +545,54 @@ int32_t orc_render_tile(const orc_scene* s, int32_t x0, int32_t y0, int32_t w, i
             }
             sum[i] = to_abi(acc);
         }
+    if (rays) *rays += nrays;
+    return 0;
+}
+
+// Diagnostic: one reference worker's draw order.  One System.Random(seed) stream; `spp` passes,
+// each over the tile row by row (Raytracer.Render, Raytracer.cs:302-320).
+// Diagnostic: one sample with its path (see get_color's `trace`, 2 * (recursion + 1) ints, -2 filled).
+int32_t orc_sample_trace(const orc_scene* s, int32_t x, int32_t y, uint64_t seed, uint64_t smp, rt_color* color,
+                         int32_t* trace)
+{
+    if (!s || s->sc.cameras.empty() || !trace) return -1;
+    const Scene& sc = s->sc;
+    std::vector<Leaf> scratch;
+    for (int i = 0; i < 2 * (sc.recursion + 1); i++) trace[i] = -2;
+    Sampler rs{rt_rng_init(seed, (uint64_t)y * (uint64_t)sc.width + (uint64_t)x, smp)};
+    Ray r = camera_ray(sc.cameras[sc.current_camera], rs, x, y);
+    int nr = 0;
+    Col c = get_color(sc, r, rs, nr, scratch, trace);
+    if (color) *color = to_abi(c);
+    return ceq(c, col(-1)) ? 1 : 0;
+}
+
+int32_t orc_render_tile_netrandom(const orc_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t spp,
+                                  int32_t seed, rt_color* sum, uint32_t* samples, uint32_t* misses, uint64_t* rays)
+{
+    if (!s || s->sc.cameras.empty() || w < 0 || h < 0 || spp < 0) return -1;
+    const Scene& sc = s->sc;
+    const Camera& cam = sc.cameras[sc.current_camera];
+    std::vector<Leaf> scratch;
+    NetRandom rs(seed);
+    uint64_t nrays = 0;
+    for (int k = 0; k < spp; k++)
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) {
+                size_t i = (size_t)x * h + y;
+                int nr = 0;
+                Ray r = camera_ray(cam, rs, x0 + x, y0 + y);
+                Col c = get_color(sc, r, rs, nr, scratch);
+                nrays += nr;
+                if (ceq(c, col(-1))) {
+                    misses[i]++;
+                } else {
+                    sum[i].r += c.r;
+                    sum[i].g += c.g;
+                    sum[i].b += c.b;
+                    samples[i]++;
+                }
+            }
     if (rays) *rays += nrays;
     return 0;
 }

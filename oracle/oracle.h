@@ -65,6 +65,18 @@ int32_t orc_render_tile(const orc_scene* s, int32_t x0, int32_t y0, int32_t w, i
                         uint64_t seed, uint64_t sample_base, rt_color* sum, uint32_t* samples,
                         uint32_t* misses, uint64_t* rays);
 
+/* Diagnostic: one sample (as orc_sample) and its path: trace[2i] = primitive met by bounce i (-1 miss),
+ * trace[2i+1] = event chosen there (1 diffuse, 2 specular, 3 specular fail, 4 transmitted,
+ * 5 emission); 2 * (recursion + 1) entries, -2 past the path's end. */
+int32_t orc_sample_trace(const orc_scene* s, int32_t x, int32_t y, uint64_t seed, uint64_t sample,
+                         rt_color* color, int32_t* trace);
+
+/* Diagnostic: the same accumulation with the draws of one reference worker thread: one .NET Core
+ * 3.1 System.Random(seed) stream, spp passes over the tile row by row (Raytracer.cs:48,302-320). */
+int32_t orc_render_tile_netrandom(const orc_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t spp,
+                                  int32_t seed, rt_color* sum, uint32_t* samples, uint32_t* misses,
+                                  uint64_t* rays);
+
 /*
  * FullRaytracer-style frame render (FullRaytracer.cs:66-72,219-229,271-302): `threads`
  * workers (0 = hardware_concurrency), TilesY = floor(sqrt(T)), TilesX = T / TilesY,

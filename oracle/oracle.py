@@ -57,6 +57,10 @@ def lib() -> C.CDLL:
             "orc_render_tile": (C.c_int32, [C.c_void_p] + [C.c_int32] * 5 + [C.c_uint64, C.c_uint64, P(rt_color),
                                                                                P(C.c_uint32), P(C.c_uint32),
                                                                                P(C.c_uint64)]),
+            "orc_sample_trace": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int32, C.c_uint64, C.c_uint64, P(rt_color),
+                                             P(C.c_int32)]),
+            "orc_render_tile_netrandom": (C.c_int32, [C.c_void_p] + [C.c_int32] * 6 + [P(rt_color), P(C.c_uint32),
+                                                                                   P(C.c_uint32), P(C.c_uint64)]),
             "orc_render_frame": (C.c_int32, [C.c_void_p, C.c_int32, C.c_uint64, C.c_int32, P(rt_color), P(C.c_uint32),
                                               P(C.c_uint32), P(C.c_uint64), P(C.c_double), P(C.c_int32)]),
             "orc_sample_output": (C.c_int32, [rt_color, C.c_uint32, C.c_uint32, rt_color, C.c_double, C.c_double]),
@@ -191,6 +195,25 @@ class OracleScene:
         assert lib().orc_render_tile(self.h, x0, y0, w, h, spp, seed, sample_base,
                                      s.ctypes.data_as(C.POINTER(rt_color)), n.ctypes.data_as(C.POINTER(C.c_uint32)),
                                      m.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(rays)) == 0
+        return s, n, m, rays.value
+
+    def sample_trace(self, x, y, seed=0, sample=0, recursion=32):
+        """Diagnostic: one sample's colour, miss flag and path [(primitive, event)] (oracle.h)."""
+        c = rt_color()
+        tr = (C.c_int32 * (2 * (recursion + 1)))()
+        miss = lib().orc_sample_trace(self.h, x, y, seed, sample, C.byref(c), tr)
+        path = [(tr[2 * i], tr[2 * i + 1]) for i in range(recursion + 1) if tr[2 * i] != -2]
+        return (c.r, c.g, c.b), bool(miss), path
+
+    def render_tile_netrandom(self, x0, y0, w, h, spp, seed=0):
+        """Diagnostic: the draws of one reference worker (.NET System.Random(seed), passes row by row)."""
+        s = np.zeros((w, h, 3), np.float64)
+        n = np.zeros((w, h), np.uint32)
+        m = np.zeros((w, h), np.uint32)
+        rays = C.c_uint64(0)
+        assert lib().orc_render_tile_netrandom(self.h, x0, y0, w, h, spp, seed,
+                                               s.ctypes.data_as(C.POINTER(rt_color)), n.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                               m.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(rays)) == 0
         return s, n, m, rays.value
 
     def render_frame(self, spp, seed=0, threads=0):

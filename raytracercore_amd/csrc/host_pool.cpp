@@ -13,10 +13,17 @@
 #include <thread>
 #include <vector>
 
+#include <pthread.h>
+#include <unistd.h>
+
 #include "host_scene.h"
 
 namespace rtc {
 namespace {
+
+// Set on the threads of a pool run (the caller and the workers): a host_run issued from inside a
+// task runs inline instead of re-entering the pool (whose run lock the caller already holds).
+thread_local bool t_in_pool = false;
 
 class Pool {
 public:
@@ -49,7 +56,9 @@ public:
             gen_++;
         }
         cv_.notify_all();
+        t_in_pool = true;
         work(task, n); // the calling thread takes tasks too
+        t_in_pool = false;
         std::unique_lock<std::mutex> g(m_);
         done_cv_.wait(g, [this] { return left_ == 0; });
         task_ = nullptr;
@@ -63,6 +72,7 @@ private:
     }
     void loop()
     {
+        t_in_pool = true;
         uint64_t seen = 0;
         for (;;) {
             const std::function<void(size_t)>* t;
@@ -101,9 +111,23 @@ int pool_width()
     return w;
 }
 
+// The pool of this process.  A fork()ed child inherits the pointer but none of the worker threads
+// (nor, if the fork came mid-run, a usable lock), so an atfork handler drops it in the child and
+// the child's first host_run builds a pool of its own.  Pools are never destroyed: workers may
+// outlive static teardown.
+std::atomic<Pool*> g_pool{nullptr};
+
+void drop_pool_in_child() { g_pool.store(nullptr); }
+
 Pool& pool()
 {
-    static Pool* p = new Pool(pool_width() - 1); // never destroyed: workers may outlive static teardown
+    Pool* p = g_pool.load();
+    if (p) return *p;
+    static const int registered = pthread_atfork(nullptr, nullptr, drop_pool_in_child);
+    (void)registered;
+    Pool* fresh = new Pool(pool_width() - 1);
+    if (g_pool.compare_exchange_strong(p, fresh)) return *fresh;
+    delete fresh; // another thread installed one first
     return *p;
 }
 
@@ -114,8 +138,8 @@ int host_threads() { return pool().size(); }
 void host_run(size_t n, const std::function<void(size_t)>& task)
 {
     if (n == 0) return;
-    if (n == 1) {
-        task(0);
+    if (n == 1 || t_in_pool) { // nested inside a pool task: inline
+        for (size_t i = 0; i < n; i++) task(i);
         return;
     }
     if (pool().run(n, task)) return;

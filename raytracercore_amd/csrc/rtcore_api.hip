@@ -1734,8 +1734,13 @@ int queue_copy(rt_scene* s, CopyPlan& plan, const void* d_src, size_t a, size_t 
 
 int consume_copies(rt_scene* s, const CopyPlan& plan, const std::function<void(const unsigned char*, size_t, size_t)>& consume)
 {
-    // chunks x S slices, handed out in order: the first tasks wait for the first chunk
-    const size_t S = (size_t)host_threads();
+    // chunks x S slices, handed out in order: the first tasks wait for the first chunk.  A slice
+    // holds at least kMinItems records, so a small tile (a few thousand pixels) is consumed on the
+    // calling thread instead of waking the pool for a few hundred records per thread.
+    constexpr size_t kMinItems = 65536;
+    size_t longest = 0;
+    for (int k = 0; k < plan.n; k++) longest = std::max(longest, plan.b[k] - plan.a[k]);
+    const size_t S = std::max<size_t>(1, std::min<size_t>((size_t)host_threads(), longest / kMinItems));
     std::atomic<int> failed{0};
     host_run((size_t)plan.n * S, [&](size_t t) {
         const size_t k = t / S, j = t % S;
@@ -2562,6 +2567,10 @@ int rt_render_tile(rt_scene* s, int32_t x0, int32_t y0, int32_t w, int32_t h, in
     }
     if (spp == 0) return RT_OK;
     HIP_TRY(hipSetDevice(s->device));
+    // A previous call that failed between its first queued copy and its consume step may have left
+    // band copies in flight on copy_stream, reading colors into stage: both are about to be
+    // reserved (maybe reallocated), so wait for them first (normally the stream is already idle).
+    if (s->copy_stream) HIP_TRY(hipStreamSynchronize(s->copy_stream));
     const size_t npix = (size_t)w * h;
     HIP_TRY(s->sum.reserve(3 * npix));
     HIP_TRY(s->samples.reserve(npix));

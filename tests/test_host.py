@@ -291,8 +291,9 @@ def test_grouped_order_records(rc, name):
     """The grouped order's records, as the scene-specialised header carries them for each camera:
     super records (a box, no primitives, skip > 0) hold the records right behind them, are not
     nested, and their box contains every record they hold; the groups together test every
-    non-plane primitive once (the flat order's count); the closed boxes of the scene are whole
-    groups' boxes (box-aware cut), so die.txt's cube is one box test."""
+    non-plane primitive once (the flat order's count).  Only under RTCORE_GROUP_BOXES=1 (the
+    box-aware cut, off by default: DESIGN §6.1) are the scene's closed boxes whole groups' boxes,
+    so that die.txt's cube is one box test; that check runs only then."""
     scene = rc.SceneLoader.from_file(rc.scene_path(name))
     flat = _group_records(rc.jit_header(scene, 0, size=(1920, 1080), grouped=False))
     assert len(flat) == 1 and flat[0]["skip"] == 0
@@ -372,3 +373,32 @@ def test_vertexnormal_rehit_test_matches_oracle(rc):
     # both outcomes occur: the residual's sign is data-dependent
     print(f"re-hit test: {hits} hits, {misses} misses, all equal to the oracle")
     assert hits > 100 and misses > 100, (hits, misses)
+
+
+def test_host_pool_survives_fork(rc):
+    """a fork()ed child inherits the persistent host pool's pointer but not its
+    worker threads.  The child's first pool-backed call must build a pool of its own instead of
+    waiting forever for workers that do not exist.  The parent runs one host-only pass large enough
+    for the pool (scene preparation of a 20,000-triangle mesh goes through parallel_for) so the pool
+    exists; a forked child then runs the same pass, which must finish and agree with the parent's."""
+    import multiprocessing as mp
+
+    from raytracercore_amd import scenes
+
+    prims = rc.SceneLoader.from_text(scenes.mesh_scene_text(101, 101)).prims
+    assert len(prims) > 20000
+    ref = rc.brute_layout(prims)
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+
+    def child():
+        q.put(rc.brute_layout(prims) == ref)
+
+    p = ctx.Process(target=child)
+    p.start()
+    p.join(120)
+    alive = p.is_alive()
+    if alive:
+        p.kill()
+    assert not alive, "forked child hung in the host pool"
+    assert p.exitcode == 0 and q.get(timeout=5)

@@ -188,13 +188,26 @@ def test_bounce_screenshot_geometry_and_uniform_exposure():
     assert ratios.std() / ratios.mean() < 0.15, ratios
 
 
-# Sphere 13 (bounce.txt:88, diffuse .9 / specular .2 at shininess 250) is the one region of app.png
-# near the 4 % bound: past the quantisation interval it reads -3.6 / -1.3 / -2.4 % (R, G, B) here
-# (1,024 oracle spp, seed 1), -3.9 / -1.8 / -2.8 % at 3,072 spp (seed 2), and its mid-interval R
-# ratio spans 0.93-0.955 over five seeds at 768 spp.  The oracle-side noise (about 1 % between
-# seeds) does not account for it; the screenshot's own noise at 4,826 spp on a glossy surface may.
-# It is held at 7 % and reported, every other region at 4 %.
-APP_REGION_TOL = {13: 0.07}
+# Sphere 13 (bounce.txt:88, diffuse .9 / specular .2 at shininess 250) is the region of app.png
+# nearest the bound: R -3.6 %, G -1.3 %, B -2.4 % beyond the quantisation interval here (1,024 spp,
+# seed 1), -3.9 % R at 3,072 spp.  In mid-interval terms the oracle is ~3.5 % darker in luminance,
+# concentrated on the sphere's upper half.  The reference's silhouette of the sphere aligns with
+# the oracle's at the viewport offset, and the screenshot's own pixel noise there matches
+# ~3,000-7,000 spp, so neither geometry nor screenshot noise explains it; the .NET System.Random
+# draw order (oracle_render_tile_netrandom), recursion and shininess variants do not move it.  It
+# stays within the 4 % bound every region is held to, and is recorded as an open parity item
+# (tools/sphere13_diag.py).
+
+
+def _app_regions(spp, seed=1):
+    d = np.load(os.path.join(GOLDEN, "screenshot_app_bounce700.npz"))
+    ref, xs, ys = d["rgb"].astype(np.int64), d["xs"], d["ys"]
+    assert tuple(d["size"]) == (700, 700) and float(d["exposure"][0]) == 1.0 and ref.shape[:2] == (175, 175)
+    got, lin, miss = _render_sparse("bounce.txt", (700, 700), xs, ys, spp, seed=seed)
+    panel = np.all(ref == d["panel"], axis=-1)  # a transparent (all-miss) pixel shows the panel grey
+    ok = (miss == 0) & ~panel & np.all(ref < 250, axis=-1)
+    rid, inner = _region_ids("bounce.txt", (700, 700), xs, ys)
+    return ref, got, lin, panel, ok, rid, inner
 
 
 def test_bounce_app_screenshot_exposure1_radiance():
@@ -202,21 +215,15 @@ def test_bounce_app_screenshot_exposure1_radiance():
     per-channel mean linear radiance of the fully covered, unsaturated pixels within 2 % of the
     oracle (1,024 spp), and region by region: every primitive with at least 200 usable pixels --
     the room's walls, floor and ceiling, the cut-out faces, sphere 13, the rotated cube's faces and
-    the Fresnel / TIR lens (20) -- within 4 % (sphere 13: APP_REGION_TOL)."""
-    d = np.load(os.path.join(GOLDEN, "screenshot_app_bounce700.npz"))
-    ref, xs, ys = d["rgb"].astype(np.int64), d["xs"], d["ys"]
-    assert tuple(d["size"]) == (700, 700) and float(d["exposure"][0]) == 1.0 and ref.shape[:2] == (175, 175)
-    got, lin, miss = _render_sparse("bounce.txt", (700, 700), xs, ys, 1024)
-    panel = np.all(ref == d["panel"], axis=-1)  # a transparent (all-miss) pixel shows the panel grey
+    the Fresnel / TIR lens (20) -- within 4 %."""
+    ref, got, lin, panel, ok, rid, inner = _app_regions(1024)
     agree = (panel != (got[..., 3] > 0)).mean()
     assert agree > 0.985, f"coverage agreement {agree:.4f}"
-    ok = (miss == 0) & ~panel & np.all(ref < 250, axis=-1)
     assert ok.sum() > 10000
     ratio = _linear_ratio(ref, lin, ok)
     print("app.png exposure-1 radiance ratio (R, G, B):", ratio, "pixels", int(ok.sum()))
     assert np.all(np.abs(ratio - 1) < 0.02), ratio
-    rid, inner = _region_ids("bounce.txt", (700, 700), xs, ys)
     regions = [(int(r), rid == r) for r in range(22)]
-    out = _check_regions("app.png", ref, lin, ok & inner, rid, regions, 0.04, tol_of=APP_REGION_TOL)
+    out = _check_regions("app.png", ref, lin, ok & inner, rid, regions, 0.04)
     # the lens, sphere 13, the floor (10), the far walls (6, 9) and a rotated-cube face must be among them
     assert {6, 9, 10, 13, 20} <= set(out) and len(out) >= 8, sorted(out)
