@@ -314,9 +314,11 @@ int rt_kernel_times(rt_scene* scene, int32_t n, float* ms);
  *   [0] BVH node visits  [1] triangle tests  [2] sphere tests           (per ray segment)
  *   [3] wave cycles in work fetch + camera ray  [4] in traversal  [5] in shading
  *   [6] wave loop iterations  [7] BVH kernels: the most traversal steps one query took (max)
+ *   [8] wide BVH kernel: traversal-stack entries written past the LDS part (global overflow)
+ *   [9] wide BVH kernel: the deepest traversal stack of any lane (max)
  * rt_scene_get_stats synchronises the device, copies min(n, RT_STATS_COUNT) counters and zeroes them.
  */
-#define RT_STATS_COUNT 8
+#define RT_STATS_COUNT 10
 int rt_scene_set_stats(rt_scene* scene, int32_t enable);
 int rt_scene_get_stats(rt_scene* scene, uint64_t* out, int32_t n);
 

@@ -441,7 +441,7 @@ class GpuRaytracer:
         return [float(v) for v in out[:n]]
 
     STAT_NAMES = ("node_visits", "tri_tests", "sph_tests", "cyc_start", "cyc_trace", "cyc_shade", "wave_iters",
-                  "max_query_steps")
+                  "max_query_steps", "stack_overflow_pushes", "max_stack_depth")
 
     def set_stats(self, enable: bool) -> None:
         """rt_scene_set_stats: run the instrumented kernel variant (profiling only)."""

@@ -575,6 +575,7 @@ __device__ __forceinline__ void wide_visit(const Node4Q& q, V3 id, V3 oi, float 
 
 struct Counters {
     unsigned nodes, tris, sphs;                                  // per lane
+    unsigned ovf_pushes, max_sp;                                 // per lane: stack entries written past the LDS part; deepest stack
     unsigned q_steps, max_steps;                                 // per lane: steps of the current / longest query
     unsigned long long cyc_start, cyc_trace, cyc_shade, iters; // per wave (uniform)
 };
@@ -1192,9 +1193,17 @@ __device__ __forceinline__ void flush_counts(unsigned long long wave_rays, const
             atomicAdd(p.stats + 5, cnt.cyc_shade);
             atomicAdd(p.stats + 6, cnt.iters);
         }
-        unsigned long long mx = cnt.max_steps;
-        for (int off = 32; off > 0; off >>= 1) mx = max(mx, (unsigned long long)__shfl_down(mx, off));
-        if (lane == 0) atomicMax(p.stats + 7, mx);
+        unsigned long long mx = cnt.max_steps, ov = cnt.ovf_pushes, ms = cnt.max_sp;
+        for (int off = 32; off > 0; off >>= 1) {
+            mx = max(mx, (unsigned long long)__shfl_down(mx, off));
+            ov += __shfl_down(ov, off);
+            ms = max(ms, (unsigned long long)__shfl_down(ms, off));
+        }
+        if (lane == 0) {
+            atomicMax(p.stats + 7, mx);
+            atomicAdd(p.stats + 8, ov);
+            atomicMax(p.stats + 9, ms);
+        }
     }
 }
 
@@ -1490,7 +1499,12 @@ __global__ void __launch_bounds__(256, WIDTH == 4 ? RT_BVH_WAVES : RT_BVH2_WAVES
                 const V3 oi = S.o * id;
                 if (WIDTH == 4) {
                     const Node4Q q = (ref & RT_HOT_BIT) ? lds_hot[ref & ~RT_HOT_BIT] : Node4Q(nodes4[ref]);
+                    [[maybe_unused]] const int sp0 = sp;
                     wide_visit<STACK>(q, id, oi, b.t, ref, sp, stk, pop);
+                    if (STATS) {
+                        cnt.ovf_pushes += (unsigned)max(0, sp - max(sp0, STACK));
+                        cnt.max_sp = max(cnt.max_sp, (unsigned)sp);
+                    }
                 } else {
                     const NodeF n = nodes[ref];
                     float tl, tr;

@@ -6,7 +6,11 @@ bounce.txt camera 0.  Prints one JSON line.
 
 The one-pass figure is taken into one reused output array (a C# caller's pinned DoubleColor[w, h],
 zeroed by the runtime, has its pages mapped); `render_tile_1spp_fresh` allocates a new numpy array
-per pass, whose first-touch page faults the call then pays."""
+per pass, whose first-touch page faults the call then pays (Raytracer.Render's own pattern,
+Raytracer.cs:305); `render_tile_1spp_recycled` is INTEGRATION.md §3's worker: a pool of arrays that
+the update loop hands back after its merge (FullRaytracer.cs:326-344), three of them in rotation
+here (the pass is queued while the previous ones wait for the merge), each allocated fresh on its
+first use and timed from then on, first touches included."""
 import json
 import os
 import sys
@@ -52,11 +56,18 @@ for spp in (256, 64, 16):
         out[f"render_tile_{spp}spp" + (f"_bands{bands}" if bands else "")] = rec
 buf = np.zeros((W, H, 3), np.float64)
 g.render_tile_1spp(0, 0, W, H, seed=1, sample_index=0, out=buf)
-for label, reuse in (("render_tile_1spp", True), ("render_tile_1spp_fresh", False)):
+for label, mode in (("render_tile_1spp", "reuse"), ("render_tile_1spp_fresh", "fresh"),
+                    ("render_tile_1spp_recycled", "pool")):
     n = 40
+    pool = []  # the arrays the merge has handed back
     t0 = time.perf_counter()
     for k in range(n):
-        g.render_tile_1spp(0, 0, W, H, seed=1, sample_index=k + 1, out=buf if reuse else None)
+        if mode == "pool":
+            arr = pool.pop(0) if len(pool) >= 3 else np.zeros((W, H, 3), np.float64)
+            g.render_tile_1spp(0, 0, W, H, seed=1, sample_index=k + 1, out=arr)
+            pool.append(arr)  # merged, returned to the pool
+        else:
+            g.render_tile_1spp(0, 0, W, H, seed=1, sample_index=k + 1, out=buf if mode == "reuse" else None)
     dt = (time.perf_counter() - t0) / n
     kt = g.kernel_times(min(n, g.KERNEL_TIME_RING))
     out[label] = {"ms_per_pass": round(dt * 1e3, 3), "msamples_per_s": round(W * H / dt / 1e6, 1),
