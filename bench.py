@@ -212,6 +212,64 @@ def cpu_baseline(cfg_name: str, threads: int = 0):
     }
 
 
+def frame_split(args) -> int:
+    """--split frame: the product's multi-GPU path, timed.  One process, rt_frame over devices
+    0..N-1 (rtcore_api.hip rt_frame_render: every device renders its interleaved 8-row band set with
+    all of the step's samples, one RCCL ncclGather over xGMI onto device 0, one copy to pinned host
+    memory, the host merge into SampleSet-order buffers).  A step is one frame of N x spp samples
+    per pixel (the same per-GPU work at every N, like the default split), and its time includes the
+    gather, the device -> host copy and the host merge: a host-buffer (PCIe-inclusive) rate, not the
+    HBM-resident `value` of the default split.  Run as ONE process (not under torchrun)."""
+    import numpy as np
+
+    import raytracercore_amd as rc
+
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("--split frame drives every GPU from one process: run it without torchrun")
+    n = args.gpus
+    if rc.device_count() < n:
+        raise SystemExit(f"--split frame: {n} GPUs asked, {rc.device_count()} visible")
+    scene_file, cam, W, H, spp = CONFIGS[args.config]
+    if args.spp > 0:
+        spp = args.spp
+    scene = load_scene(rc, scene_file)
+    frame = rc.GpuFrame(scene, cam, n_gpus=n, size=(W, H))
+    frame_spp = spp * n
+    acc = (np.zeros((W, H, 3), np.float64), np.zeros((W, H), np.uint32), np.zeros((W, H), np.uint32))
+    for k in range(args.warmup):
+        frame.render(frame_spp, args.seed, k * frame_spp, out=acc)
+    rays = 0
+    step_ms = []
+    t0 = time.perf_counter()
+    for k in range(args.warmup, args.warmup + args.steps):
+        s0 = time.perf_counter()
+        rays += frame.render(frame_spp, args.seed, k * frame_spp, out=acc)[3]
+        step_ms.append((time.perf_counter() - s0) * 1e3)
+    elapsed = time.perf_counter() - t0
+    expect = frame_spp * (args.warmup + args.steps)
+    tot = acc[1].astype(np.int64) + acc[2].astype(np.int64)
+    if not np.all(tot == expect):
+        raise SystemExit(f"sample bookkeeping mismatch: {np.unique(tot)} != {expect}")
+    frame.close()
+    out = {
+        "metric": "Mrays/sec (primary+secondary), multi-GPU product path (rt_frame, host buffers)",
+        "value": round(rays / elapsed / 1e6, 2), "unit": "Mrays/s", "n_gpus": n, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: the reference's own scene file (tests/golden/scenes) with seeded camera samples",
+        "config": {"workload": f"{scene_file} camera {cam} {W}x{H} x {spp} spp per GPU per step",
+                   "parallelism": f"rt_frame: one process, {n} GPU(s), interleaved 8-row band sets, "
+                                  + ("one ncclGather over xGMI per step" if n > 1 else "no collective")
+                                  + ", merge into host SampleSet buffers"},
+        "step_ms_min": round(min(step_ms), 3), "step_ms_max": round(max(step_ms), 3),
+        "roofline": None,
+        "note": "host-buffer rate (includes the gather, the device -> host copy of 32 B per pixel and the host "
+                "merge); the HBM-resident rate of the same per-GPU work is the default split's `value`",
+    }
+    print(json.dumps(out), flush=True)
+    return 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -223,9 +281,14 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--split", default="bands", choices=["bands", "samples"],
-                    help="multi-GPU split: interleaved row bands + gather (default) or sample ranges + reduce")
+    ap.add_argument("--split", default="bands", choices=["bands", "samples", "frame"],
+                    help="multi-GPU split: interleaved row bands + gather (default) or sample ranges + reduce, "
+                         "one rank per GPU over torch.distributed; or `frame`: ONE process drives --gpus GPUs "
+                         "through the library's own rt_frame (the product path a C# host calls: band sets, "
+                         "ncclGather to device 0, merge into host SampleSet buffers)")
     args = ap.parse_args()
+    if args.split == "frame":
+        return frame_split(args)
 
     import numpy as np
     import torch

@@ -350,6 +350,17 @@ int rt_render_bands_device(rt_scene* scene, int32_t band, int32_t band_stride, i
                            unsigned long long* d_rays, void* stream);
 /* Rows of a frame of `height` rows in band set (band, band_stride, band_offset); host only. */
 int rt_band_rows(int32_t height, int32_t band, int32_t band_stride, int32_t band_offset);
+/* Rows of the tallest band set of the split (band, band_stride, *): a gather slot's plane is
+ * this x width (host only). */
+int rt_band_slot_rows(int32_t height, int32_t band, int32_t band_stride);
+/* Host only: rt_frame_render's merge step for one device's gathered slot -- the slot (Σr | Σg | Σb
+ * fp64 planes, then samples and misses u32 planes, each `plane` elements, row-major over the band
+ * set's rows in frame order) added into frame buffers in the x*height + y order.  Exposed so that
+ * the single-process frame path's band layout can be checked against a per-rank host's (the
+ * torch.distributed split of bench.py, raytracercore_amd/sharding.py) without devices. */
+int rt_scatter_band_slot(const void* slot, uint64_t plane, int32_t width, int32_t height, int32_t band,
+                         int32_t band_stride, int32_t band_offset, rt_color* sum_rgb, uint32_t* samples,
+                         uint32_t* misses);
 
 /*
  * Persistent whole-frame renderer over devices 0..n_gpus-1 of this process (replaces the

@@ -156,6 +156,9 @@ def load_library(path: str = "") -> C.CDLL:
         "rt_render_bands_device": (C.c_int, [C.c_void_p] + [C.c_int32] * 4 + [C.c_uint64, C.c_uint64] +
                                    [C.c_void_p] * 3 + [C.c_uint64, C.c_void_p, C.c_void_p]),
         "rt_band_rows": (C.c_int, [C.c_int32] * 4),
+        "rt_band_slot_rows": (C.c_int, [C.c_int32] * 3),
+        "rt_scatter_band_slot": (C.c_int, [C.c_void_p, C.c_uint64] + [C.c_int32] * 5 + [P(rt_color), P(C.c_uint32),
+                                                                                       P(C.c_uint32)]),
         "rt_frame_create": (C.c_int, [P(rt_scene_params), P(rt_prim), C.c_int32, P(rt_camera), C.c_int32,
                                       P(C.c_void_p)]),
         "rt_frame_set_camera": (C.c_int, [C.c_void_p, P(rt_camera)]),
@@ -517,6 +520,26 @@ def band_rows_count(height: int, band: int, band_stride: int, band_offset: int) 
     n = load_library().rt_band_rows(height, band, band_stride, band_offset)
     _check(min(n, 0))
     return n
+
+
+def band_slot_rows(height: int, band: int, band_stride: int) -> int:
+    """rt_band_slot_rows: rows of the tallest band set of the split (host only)."""
+    n = load_library().rt_band_slot_rows(height, band, band_stride)
+    _check(min(n, 0))
+    return n
+
+
+def scatter_band_slot(slot: np.ndarray, plane: int, width: int, height: int, band: int, band_stride: int,
+                      band_offset: int, out) -> None:
+    """rt_scatter_band_slot (host only): rt_frame_render's merge of one device's gathered slot (a
+    float64 array of 4 * plane: sum planes, then the samples / misses u32 planes) into
+    (sum[W,H,3], samples[W,H], misses[W,H])."""
+    s, n, m = out
+    slot = np.ascontiguousarray(slot, dtype=np.float64)
+    _check(load_library().rt_scatter_band_slot(slot.ctypes.data_as(C.c_void_p), plane, width, height, band,
+                                               band_stride, band_offset, s.ctypes.data_as(C.POINTER(rt_color)),
+                                               n.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                               m.ctypes.data_as(C.POINTER(C.c_uint32))))
 
 
 def render_frame_multi(scene: ParsedScene, camera_index: int, n_gpus: int, spp: int, seed: int = 0,

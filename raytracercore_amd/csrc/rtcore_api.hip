@@ -2919,6 +2919,30 @@ int rt_band_rows(int32_t height, int32_t band, int32_t band_stride, int32_t band
     return band_set_rows(height, band, band_stride, band_offset);
 }
 
+int rt_band_slot_rows(int32_t height, int32_t band, int32_t band_stride)
+{
+    if (height < 0 || band <= 0 || band_stride <= 0) {
+        set_error("rt_band_slot_rows: bad argument");
+        return RT_ERR_ARG;
+    }
+    return band_slot_rows(height, band, band_stride);
+}
+
+int rt_scatter_band_slot(const void* slot, uint64_t plane, int32_t width, int32_t height, int32_t band,
+                         int32_t band_stride, int32_t band_offset, rt_color* sum_rgb, uint32_t* samples,
+                         uint32_t* misses)
+{
+    if (!slot || !sum_rgb || !samples || !misses || width <= 0 || height <= 0 || band <= 0 || band_stride <= 0 ||
+        band_offset < 0 || band_offset >= band_stride ||
+        plane < (uint64_t)band_set_rows(height, band, band_stride, band_offset) * (uint64_t)width) {
+        set_error("rt_scatter_band_slot: bad argument");
+        return RT_ERR_ARG;
+    }
+    scatter_band_set(static_cast<const unsigned char*>(slot), (size_t)plane, width, height, band, band_stride,
+                     band_offset, sum_rgb, samples, misses);
+    return RT_OK;
+}
+
 int rt_frame_create(const rt_scene_params* params, const rt_prim* prims, int32_t n_prims, const rt_camera* camera,
                     int32_t n_gpus, rt_frame** out)
 {

@@ -187,3 +187,41 @@ def test_sample_bases_disjoint():
             rng = set(range(b, b + 256))
             assert not (seen & rng)
             seen |= rng
+
+
+@pytest.mark.parametrize("h,w,world", [(27, 5, 2), (27, 5, 3), (37, 11, 2), (40, 7, 3), (1080, 16, 3)])
+def test_frame_path_layout_matches_sharding(rc, h, w, world):
+    """The two multi-GPU paths share one band layout.  The product path is the
+    library's rt_frame (one process drives every GPU: render each band set into a gather slot,
+    ncclGather to device 0, scatter on the host -- rt_frame_render); bench.py's per-rank path
+    renders the same slots through rt_render_bands_device and scatters them with sharding.py.
+    Here random slots in that layout are scattered both ways and must give the same frame bit for
+    bit: the library's rt_scatter_band_slot (rt_frame_render's merge, [x, y] order) against
+    sharding.scatter_slots (row-major planes); and both size the slot alike."""
+    torch = pytest.importorskip("torch")
+    plane = sharding.slot_rows(h, world) * w
+    assert rc.band_slot_rows(h, sharding.BAND, world) * w == plane
+    gen = torch.Generator().manual_seed(h * 100 + world)
+    slots = []
+    for r in range(world):
+        slot = torch.zeros(4 * plane, dtype=torch.float64)
+        s_, n_, m_ = sharding.slot_views(slot, plane)
+        k = len(band_rows(h, world, r)) * w  # the set's rows; the rest of each plane stays unused (0)
+        s_.view(3, plane)[:, :k] = torch.rand(3, k, generator=gen, dtype=torch.float64)
+        n_[:k] = torch.randint(0, 1000, (k,), generator=gen, dtype=torch.int32)
+        m_[:k] = torch.randint(0, 1000, (k,), generator=gen, dtype=torch.int32)
+        slots.append(slot)
+    # the per-rank host's merge (bench.py rank 0)
+    f_sum = torch.zeros(3 * h * w, dtype=torch.float64)
+    f_n = torch.zeros(h * w, dtype=torch.int32)
+    f_m = torch.zeros(h * w, dtype=torch.int32)
+    sharding.scatter_slots(f_sum, f_n, f_m, slots, sharding.row_index(h, world), w, plane)
+    # the frame path's merge, into SampleSet[w, h] order
+    out = (np.zeros((w, h, 3)), np.zeros((w, h), np.uint32), np.zeros((w, h), np.uint32))
+    for r in range(world):
+        rc.scatter_band_slot(slots[r].numpy(), plane, w, h, sharding.BAND, world, r, out)
+    assert np.array_equal(out[0].transpose(2, 1, 0), f_sum.view(3, h, w).numpy())
+    assert np.array_equal(out[1].T.astype(np.int64), f_n.view(h, w).numpy().astype(np.int64))
+    assert np.array_equal(out[2].T.astype(np.int64), f_m.view(h, w).numpy().astype(np.int64))
+    # every frame row owned by exactly one rank
+    assert np.all(out[1].T.sum(axis=1) == f_n.view(h, w).numpy().sum(axis=1))

@@ -54,6 +54,21 @@ PATCHES = {
     # wide BVH visit without the child-count test (empty slots have inverted boxes; C4 -0.6 %, kept for safety)
     "WIDE_NO_NC": [("        D = ((K < nc) & (tmin <= fminf(tmax * 1.00000024f, tmax_best))) ? tmin : __builtin_huge_valf();         \\\n",
                     "        D = (tmin <= fminf(tmax * 1.00000024f, tmax_best)) ? tmin : __builtin_huge_valf();         \\\n")],
+    # work items of one wave: the samples of one pixel (chunk-major) instead of one sample of the
+    # 64 pixels of an 8x8 block (C4 ray-coherence probe: a wave's primary rays then meet one point)
+    "SAMPLE_MAJOR": [("                const unsigned q = L.item & 63u, t = L.item >> 6;\n"
+                      "                const int c = (int)(t & (unsigned)(p.n_chunks - 1));\n",
+                      "                const unsigned q = (L.item >> p.log2_chunks) & 63u, t = ((L.item >> (p.log2_chunks + 6)) << p.log2_chunks) | (L.item & (unsigned)(p.n_chunks - 1));\n"
+                      "                const int c = (int)(t & (unsigned)(p.n_chunks - 1));\n")],
+    # leaf step: a record past the leaf's end is loaded from the leaf's first record instead (same
+    # instructions, no spare line): the cost of the spare records' lines
+    "NO_SPARE_LINE": [("        r[j][0] = rows[3 * (k + j)];\n"
+                       "        r[j][1] = rows[3 * (k + j) + 1];\n"
+                       "        r[j][2] = rows[3 * (k + j) + 2];\n",
+                       "        const int kk = (j == 0 || k + j < kend) ? k + j : k;\n"
+                       "        r[j][0] = rows[3 * kk];\n"
+                       "        r[j][1] = rows[3 * kk + 1];\n"
+                       "        r[j][2] = rows[3 * kk + 2];\n")],
     # no literal folding of zero scene fields in the specialised build
     "NO_KFOLD": [("    return __builtin_constant_p(c) && c == 0.0f;\n", "    return false;\n")],
 }

@@ -8,6 +8,10 @@
    waves per SIMD; its hits must equal the logged ones.
 3. Printed: the megakernel's timed rate at the bench launch (64 spp) and the trace-only rate,
    both in Grays/s, and the trace-only kernel's lane-slot split.
+4. Round 5 (ray coherence): the same queries sorted the way a ray-binning step
+   would group them -- by direction octant then origin Morton code, by a finer direction bin
+   (cube-map face x 8 x 8) then origin, and by origin then direction -- bound what regrouping the
+   megakernel's secondary rays could gain in the traversal itself.
 usage: python tools/trace_only.py [SPP]
 """
 import ctypes as C
@@ -73,6 +77,32 @@ def main():
     key_bounce = logged[:, 2, 2].view(torch.int32).to(torch.int64)
     orders["bounce_then_pixel"] = torch.argsort(key_bounce * (W * H) + key_pix)
     orders["pixel_then_bounce"] = torch.argsort(key_pix * 16 + key_bounce)
+    # coherent orders: origin Morton code (10 bits per axis over the logged origins' bounds) and
+    # direction bins (octant, or cube-map face x 8 x 8 cells)
+    o = logged[:, 0, :3]
+    d = logged[:, 1, :3]
+    lo, hi = o.min(0).values, o.max(0).values
+    q = ((o - lo) / (hi - lo).clamp_min(1e-9) * 1023).clamp(0, 1023).to(torch.int64)
+
+    def spread(v):  # 10 bits -> every third bit of 30
+        v = (v | (v << 16)) & 0x030000FF
+        v = (v | (v << 8)) & 0x0300F00F
+        v = (v | (v << 4)) & 0x030C30C3
+        return (v | (v << 2)) & 0x09249249
+
+    morton = spread(q[:, 0]) | (spread(q[:, 1]) << 1) | (spread(q[:, 2]) << 2)
+    octant = ((d[:, 0] < 0).to(torch.int64) | ((d[:, 1] < 0).to(torch.int64) << 1) |
+              ((d[:, 2] < 0).to(torch.int64) << 2))
+    ad = d.abs()
+    face = ad.argmax(1)
+    major = ad.gather(1, face[:, None])[:, 0].clamp_min(1e-9)
+    sgn = (d.gather(1, face[:, None])[:, 0] < 0).to(torch.int64)
+    uv = torch.stack([d[:, (face + 1) % 3], d[:, (face + 2) % 3]], 1) / major[:, None]  # in [-1, 1]
+    cell = ((uv + 1) * 4).clamp(0, 7.999).to(torch.int64)
+    dirbin = ((face * 2 + sgn) * 8 + cell[:, 0]) * 8 + cell[:, 1]  # 384 bins
+    orders["octant_then_origin"] = torch.argsort((octant << 30) | morton)
+    orders["dirbin_then_origin"] = torch.argsort((dirbin << 30) | morton)
+    orders["origin_then_octant"] = torch.argsort((morton << 3) | octant)
     base_log = log
 
     def trace(order, waves, rays):
