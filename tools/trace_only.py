@@ -97,7 +97,8 @@ def main():
     face = ad.argmax(1)
     major = ad.gather(1, face[:, None])[:, 0].clamp_min(1e-9)
     sgn = (d.gather(1, face[:, None])[:, 0] < 0).to(torch.int64)
-    uv = torch.stack([d[:, (face + 1) % 3], d[:, (face + 2) % 3]], 1) / major[:, None]  # in [-1, 1]
+    uv = torch.stack([d.gather(1, ((face + 1) % 3)[:, None])[:, 0], d.gather(1, ((face + 2) % 3)[:, None])[:, 0]],
+                     1) / major[:, None]  # in [-1, 1]
     cell = ((uv + 1) * 4).clamp(0, 7.999).to(torch.int64)
     dirbin = ((face * 2 + sgn) * 8 + cell[:, 0]) * 8 + cell[:, 1]  # 384 bins
     orders["octant_then_origin"] = torch.argsort((octant << 30) | morton)
@@ -126,9 +127,13 @@ def main():
                                        "all": round(st[2] / n, 3)}}
 
     out["trace_only"] = []
+    pick = os.environ.get("TRACE_ORDERS")  # e.g. "pixel_then_bounce,octant_then_origin" (PMC passes)
+    wv = [int(v) for v in os.environ.get("TRACE_WAVES", "6,8").split(",")]
     for oname, perm in orders.items():
+        if pick and oname not in pick.split(","):
+            continue
         rays = base_log[: n * 12] if perm is None else base_log[: n * 12].view(n, 12)[perm].contiguous().view(-1)
-        for waves in (6, 8):
+        for waves in wv:
             out["trace_only"].append(trace(oname, waves, rays))
     print(json.dumps(out, indent=1))
     gpu.close()
