@@ -69,6 +69,37 @@ PATCHES = {
                        "        r[j][0] = rows[3 * kk];\n"
                        "        r[j][1] = rows[3 * kk + 1];\n"
                        "        r[j][2] = rows[3 * kk + 2];\n")],
+    # leaf rows loaded non-temporally (streamed past L2, so the nodes stay there longer)
+    "NT_ROWS": [("        r[j][0] = rows[3 * (k + j)];\n"
+                 "        r[j][1] = rows[3 * (k + j) + 1];\n"
+                 "        r[j][2] = rows[3 * (k + j) + 2];\n",
+                 "        {\n"
+                 "            typedef float ntf4 __attribute__((ext_vector_type(4)));\n"
+                 "            typedef __attribute__((address_space(1))) const ntf4 gf4;\n"
+                 "            gf4* g = (gf4*)(uintptr_t)(rows + 3 * (k + j));\n"
+                 "            ntf4 a0 = __builtin_nontemporal_load(g), a1 = __builtin_nontemporal_load(g + 1),\n"
+                 "                 a2 = __builtin_nontemporal_load(g + 2);\n"
+                 "            r[j][0] = make_float4(a0.x, a0.y, a0.z, a0.w);\n"
+                 "            r[j][1] = make_float4(a1.x, a1.y, a1.z, a1.w);\n"
+                 "            r[j][2] = make_float4(a2.x, a2.y, a2.z, a2.w);\n"
+                 "        }\n")],
+    # wide nodes loaded non-temporally
+    "NT_NODES": [("                    const Node4Q q = (ref & RT_HOT_BIT) ? lds_hot[ref & ~RT_HOT_BIT] : Node4Q(nodes4[ref]);\n"
+                  "                    [[maybe_unused]] const int sp0 = sp;\n",
+                  "                    Node4Q q;\n"
+                  "                    if (ref & RT_HOT_BIT) q = lds_hot[ref & ~RT_HOT_BIT];\n"
+                  "                    else {\n"
+                  "                        typedef float ntf4 __attribute__((ext_vector_type(4)));\n"
+                  "                        typedef __attribute__((address_space(1))) const ntf4 gf4;\n"
+                  "                        gf4* g = (gf4*)(uintptr_t)(nodes4 + ref);\n"
+                  "                        ntf4 a0 = __builtin_nontemporal_load(g), a1 = __builtin_nontemporal_load(g + 1),\n"
+                  "                             a2 = __builtin_nontemporal_load(g + 2), a3 = __builtin_nontemporal_load(g + 3);\n"
+                  "                        q.a = make_float4(a0.x, a0.y, a0.z, a0.w);\n"
+                  "                        q.b = make_float4(a1.x, a1.y, a1.z, a1.w);\n"
+                  "                        q.c = make_float4(a2.x, a2.y, a2.z, a2.w);\n"
+                  "                        q.d = make_float4(a3.x, a3.y, a3.z, a3.w);\n"
+                  "                    }\n"
+                  "                    [[maybe_unused]] const int sp0 = sp;\n")],
     # no literal folding of zero scene fields in the specialised build
     "NO_KFOLD": [("    return __builtin_constant_p(c) && c == 0.0f;\n", "    return false;\n")],
 }
