@@ -56,3 +56,14 @@ def test_bench_two_ranks_one_device():
     mg = d["multi_gpu"]  # the N > 1 line explains itself: ranks' kernel times, collective and merge phases
     assert mg["world_size"] == 2 and len(mg["kernel_ms_per_rank"]) == 2
     assert mg["kernel_ms_min"] <= mg["kernel_ms_max"] and mg["gather_ms"] >= 0 and mg["scatter_ms"] >= 0
+
+
+def test_bench_frame_split_single_process():
+    """`--split frame`: the product multi-GPU path (rt_frame, one process) timed at N = 1; one JSON
+    line, the per-GPU workload, and the sample bookkeeping check inside bench.py passed (rc 0)."""
+    r = subprocess.run([sys.executable, "bench.py", "--split", "frame", "--gpus", "1", "--steps", "2", "--warmup", "1",
+                        "--spp", "8"], cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 1 and d["value"] > 0 and d["steps"] == 2 and d["scaling"] == "weak"
+    assert "rt_frame" in d["config"]["parallelism"] and d["config"]["workload"].startswith("bounce.txt")
