@@ -189,12 +189,12 @@ bool slab(const Box3& b, const Ray& r, const double inv[3], double tmax, double&
 
 // mode 0: children sorted by entry distance; 1: octant slot order (slot ^ o)
 int trace(const Wide& W, const SahBvh& b2, const std::vector<HostPrim>& H, const Ray& r, int mode, double& t_best,
-          Stats& st)
+          Stats& st, int best_in = -1, double t_in = INFINITY)
 {
     const double inv[3] = {1 / r.d[0], 1 / r.d[1], 1 / r.d[2]};
     const int oct = (r.d[0] < 0 ? 1 : 0) | (r.d[1] < 0 ? 2 : 0) | (r.d[2] < 0 ? 4 : 0);
-    int best = -1;
-    t_best = INFINITY;
+    int best = best_in;
+    t_best = t_in;
     std::vector<int> stack{W.root};
     while (!stack.empty()) {
         const int ref = stack.back();
@@ -250,6 +250,18 @@ int main(int argc, char** argv)
     const int n_bounces = argc > 6 ? atoi(argv[6]) : 2;
     const std::vector<HostPrim> H = prepare_prims(ps.prims.data(), (int)ps.prims.size());
     const SahBvh b2 = build_sah_bvh(H, H.size() > 256 ? 3 : 2);
+    // round 5: the axis-aligned rectangles (the room's and the light box's faces: box records in the
+    // brute-force kernels) taken out of the tree and tested first, their hit the traversal's
+    // initial best
+    std::vector<HostPrim> Hin, Hrect;
+    for (const HostPrim& p : H) ((p.kind == RT_PRIM_TRIANGLE && (p.flags & F_MIRROR)) ? Hrect : Hin).push_back(p);
+    const SahBvh b2in = build_sah_bvh(Hin, Hin.size() > 256 ? 3 : 2);
+    Wide w4in;
+    w4in.n2 = &b2in.nodes;
+    w4in.width = 4;
+    w4in.root = w4in.emit(0);
+    Stats s4in;
+    double rect_tests = 0;
     Wide w4, w8s, w8o;
     w4.n2 = w8s.n2 = w8o.n2 = &b2.nodes;
     w4.width = 4;
@@ -280,6 +292,21 @@ int main(int argc, char** argv)
             for (int bounce = 0; bounce <= n_bounces; bounce++) {
                 double t4, t8, t8o;
                 const int h4 = trace(w4, b2, H, r, 0, t4, s4);
+                {
+                    int bi = -1;
+                    double bt = INFINITY;
+                    for (size_t k = 0; k < Hrect.size(); k++) {
+                        double t;
+                        rect_tests++;
+                        if (hit_prim(Hrect[k], r, t) && t < bt) {
+                            bt = t;
+                            bi = (int)k;
+                        }
+                    }
+                    double tin;
+                    trace(w4in, b2in, Hin, r, 0, tin, s4in, bi, bt);
+                    s4in.rays++;
+                }
                 trace(w8s, b2, H, r, 0, t8, s8s);
                 trace(w8o, b2, H, r, 1, t8o, s8o);
                 s4.rays++;
@@ -328,6 +355,8 @@ int main(int argc, char** argv)
                     s.prims / s.rays, s.rays);
     };
     rep("4-wide, distance-sorted", s4);
+    rep("4-wide, rects out + first", s4in);
+    std::printf("  rectangles out of the tree: %zu, tested per ray segment: %.2f\n", Hrect.size(), rect_tests / s4in.rays);
     rep("8-wide, distance-sorted", s8s);
     rep("8-wide, octant order", s8o);
     return 0;
