@@ -60,12 +60,15 @@ def scene_counts(scene):
 def flops_per_ray(st) -> float:
     """SURVEY.md §8(d) compute view, exactly: 20*N_node + 45*N_tri + 30*N_sph + 150 FLOP per ray segment,
     with N_* the node visits / primitive tests per ray segment measured by the instrumented kernel
-    (rectangles, boxes' faces and frame faces count as triangles; C2: 45*19 + 30*3 + 150 = 1095)."""
-    return 20.0 * st["nodes"] + 45.0 * st["tris"] + 30.0 * st["sphs"] + 150.0
+    (rectangles, boxes' faces and frame faces count as triangles, the BVH order's outer faces too;
+    C2: 45*19 + 30*3 + 150 = 1095)."""
+    return 20.0 * st["nodes"] + 45.0 * (st["tris"] + st.get("outer", 0.0)) + 30.0 * st["sphs"] + 150.0
 
 
 def bytes_per_ray(st, scene) -> float:
-    """SURVEY.md §8(d) B_ray: 32 + 16 + 32*N_node + 48*N_tri + 16*N_sph (+144 transformed) + 48."""
+    """SURVEY.md §8(d) B_ray: 32 + 16 + 32*N_node + 48*N_tri + 16*N_sph (+144 transformed) + 48.
+    The BVH kernels' outer faces (st["outer"]) are not in N_tri here: their records are wave-uniform
+    scalar loads, one per wave rather than per ray, so they add no per-ray memory traffic."""
     n_tri, n_sph, n_pln, n_xf = scene_counts(scene)
     xf_share = n_xf / n_sph if n_sph else 0.0
     return 32 + 16 + 32.0 * st["nodes"] + 48.0 * st["tris"] + st["sphs"] * (16.0 + 144.0 * xf_share) + 48
@@ -134,6 +137,7 @@ def path_stats(gpu, W, H, spp, seed, d_rays):
     # kernel with s_memtime around sections whose loads are still in flight, it disagreed with the
     # duplicated-section costs of the timed kernel)
     out = {"nodes": st["node_visits"] / rays, "tris": st["tri_tests"] / rays, "sphs": st["sph_tests"] / rays,
+           "outer": st["outer_tests"] / rays,
            "wave_iters_per_ray": round(st["wave_iters"] * 64 / rays, 4), "lane_slots": None}
     if gpu.info().traversal in (2, 3):  # BVH kernels: the three "cycle" counters count lane slots
         slots = st["wave_iters"] * 64
@@ -518,7 +522,7 @@ def main() -> int:
             "rays_per_sample": round(total_rays / total_samples, 4),
             "kernel_ms": round(avg_ms, 3),
             "roofline": roofline(args.config, fpr, bpr, my_rays_per_step, avg_ms, counters),
-            "path_stats": {"per_ray": {k: round(st[k], 3) for k in ("nodes", "tris", "sphs")},
+            "path_stats": {"per_ray": {k: round(st[k], 3) for k in ("nodes", "tris", "sphs", "outer")},
                            "flop_per_ray": round(fpr, 1), "bytes_per_ray": round(bpr, 1),
                            "rays_per_launch": round(my_rays_per_step),
                            "lane_slots_per_ray": st["wave_iters_per_ray"],

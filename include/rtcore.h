@@ -173,8 +173,10 @@ typedef enum rt_bvh_builder {
    it came from the cache), [17] 1 if it came from the in-process or on-disk cache,
    [18] primitives per group of the grouped brute-force order (fixed at creation: 8 when the
    scene-specialised build was on then, else 4); [19] leaves of the wide tree, [20] of them compact
-   (primitives of one kind and one set of test flags, read as 48-B records) */
-#define RT_BUILD_STATS_COUNT 21
+   (primitives of one kind and one set of test flags, read as 48-B records); [21] outer
+   primitives: axis-aligned rectangles the BVH leaves out and tests as one group of rects and
+   closed boxes when a query ends (host builder, scenes of more than 4096 BVH primitives) */
+#define RT_BUILD_STATS_COUNT 22
 
 /* ---------------------------------------------------------------- library ---- */
 int rt_abi_version(void);
@@ -186,6 +188,8 @@ int rt_last_error(char* buf, int32_t cap);
 int rt_scene_create(const rt_scene_params* params, const rt_prim* prims, int32_t n_prims,
                     int32_t device, rt_scene** out_scene);
 int rt_scene_set_camera(rt_scene* scene, const rt_camera* camera);
+/* RT_ERR_ARG (the scene's mode unchanged) for a mode the scene cannot run: brute force over more
+   than 65535 triangles or 32767 spheres, a BVH deeper than the kernel's traversal stack. */
 int rt_scene_set_traversal(rt_scene* scene, int32_t traversal);
 int rt_scene_get_info(const rt_scene* scene, rt_scene_info* info);
 void rt_scene_destroy(rt_scene* scene);
@@ -316,9 +320,11 @@ int rt_kernel_times(rt_scene* scene, int32_t n, float* ms);
  *   [6] wave loop iterations  [7] BVH kernels: the most traversal steps one query took (max)
  *   [8] wide BVH kernel: traversal-stack entries written past the LDS part (global overflow)
  *   [9] wide BVH kernel: the deepest traversal stack of any lane (max)
+ *   [10] BVH kernels: faces of the outer records tested (rectangles and closed boxes' faces left
+ *        out of the tree, build statistic [21]; wave-uniform records, not in [1])
  * rt_scene_get_stats synchronises the device, copies min(n, RT_STATS_COUNT) counters and zeroes them.
  */
-#define RT_STATS_COUNT 10
+#define RT_STATS_COUNT 11
 int rt_scene_set_stats(rt_scene* scene, int32_t enable);
 int rt_scene_get_stats(rt_scene* scene, uint64_t* out, int32_t n);
 

@@ -32,7 +32,7 @@ RT_BVH_BUILDER_AUTO, RT_BVH_BUILDER_HOST, RT_BVH_BUILDER_GPU = 0, 1, 2
 BUILD_STAT_NAMES = ("prepare_ms", "bvh_ms", "upload_ms", "gpu_build_ms", "ploc_rounds", "wide_nodes", "stack_need",
                     "flat_rects", "flat_boxes", "flat_frames", "flat_frame_boxes", "flat_frame_rects", "flat_tris",
                     "flat_spheres", "hot_nodes", "jit_status", "jit_compile_ms", "jit_cached", "group_max",
-                    "wide_leaves", "compact_leaves")
+                    "wide_leaves", "compact_leaves", "outer_prims")
 
 
 def set_jit(on: bool) -> None:
@@ -444,7 +444,7 @@ class GpuRaytracer:
         return [float(v) for v in out[:n]]
 
     STAT_NAMES = ("node_visits", "tri_tests", "sph_tests", "cyc_start", "cyc_trace", "cyc_shade", "wave_iters",
-                  "max_query_steps", "stack_overflow_pushes", "max_stack_depth")
+                  "max_query_steps", "stack_overflow_pushes", "max_stack_depth", "outer_tests")
 
     def set_stats(self, enable: bool) -> None:
         """rt_scene_set_stats: run the instrumented kernel variant (profiling only)."""

@@ -175,7 +175,7 @@ void sah_prim_box(const HostPrim& p, float lo[3], float hi[3])
     }
 }
 
-SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf, bool full)
+SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf, bool full, const std::vector<char>* skip)
 {
     SahBvh out;
     SahBuilder b;
@@ -183,7 +183,7 @@ SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf, bool full
     b.full = full;
     for (int i = 0; i < (int)prims.size(); i++) {
         const HostPrim& p = prims[i];
-        if (p.kind == RT_PRIM_PLANE) continue;
+        if (p.kind == RT_PRIM_PLANE || (skip && (*skip)[i])) continue;
         Ref r;
         r.prim = i;
         sah_prim_box(p, r.box.lo, r.box.hi);

@@ -102,7 +102,9 @@ struct SahBvh {
     std::vector<SahFullNode> full; // with build_sah_bvh(..., full = true): the tree below the leaves too
     int full_root = 0;
 };
-SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf, bool full = false);
+// skip: primitives (by index) left out of the tree, besides the planes
+SahBvh build_sah_bvh(const std::vector<HostPrim>& prims, int max_leaf, bool full = false,
+                     const std::vector<char>* skip = nullptr);
 // fp32 box of a primitive for the fast-path BVHs: the fp64 bounds padded by 2^-20 relative and
 // rounded outward (used by the host and the GPU builder alike)
 void sah_prim_box(const HostPrim& p, float lo[3], float hi[3]);

@@ -576,6 +576,7 @@ __device__ __forceinline__ void wide_visit(const Node4Q& q, V3 id, V3 oi, float 
 struct Counters {
     unsigned nodes, tris, sphs;                                  // per lane
     unsigned ovf_pushes, max_sp;                                 // per lane: stack entries written past the LDS part; deepest stack
+    unsigned outer;                                              // per lane: faces of the BVH order's outer group tested
     unsigned q_steps, max_steps;                                 // per lane: steps of the current / longest query
     unsigned long long cyc_start, cyc_trace, cyc_shade, iters; // per wave (uniform)
 };
@@ -1193,16 +1194,18 @@ __device__ __forceinline__ void flush_counts(unsigned long long wave_rays, const
             atomicAdd(p.stats + 5, cnt.cyc_shade);
             atomicAdd(p.stats + 6, cnt.iters);
         }
-        unsigned long long mx = cnt.max_steps, ov = cnt.ovf_pushes, ms = cnt.max_sp;
+        unsigned long long mx = cnt.max_steps, ov = cnt.ovf_pushes, ms = cnt.max_sp, ot = cnt.outer;
         for (int off = 32; off > 0; off >>= 1) {
             mx = max(mx, (unsigned long long)__shfl_down(mx, off));
             ov += __shfl_down(ov, off);
             ms = max(ms, (unsigned long long)__shfl_down(ms, off));
+            ot += __shfl_down(ot, off);
         }
         if (lane == 0) {
             atomicMax(p.stats + 7, mx);
             atomicAdd(p.stats + 8, ov);
             atomicMax(p.stats + 9, ms);
+            atomicAdd(p.stats + 10, ot);
         }
     }
 }
@@ -1317,6 +1320,28 @@ __global__ void __launch_bounds__(256, CULL ? RT_GROUPED_WAVES : RT_PATH_WAVES)
                 const XformF*, const MatF*, const float4*)
 {
     path_body<CULL, LDS, STATS, VN>(camp, pp); // the other arguments are the BVH kernels' (same launch)
+}
+
+// The BVH order's outer group (DevScene::groups_bvh): the world rects and closed boxes left out of
+// the tree, tested by the lanes whose query ended, as the brute-force kernels test a group.
+template <bool STATS, class GroupP, class RectP, class BoxP>
+__device__ __forceinline__ void test_outer(GroupP groups, RectP rects, BoxP boxes, V3 o, V3 d, int prev, Best& b,
+                                           unsigned& n_tests)
+{
+    const V3 id = v3(slab_rcp_lean(d.x), slab_rcp_lean(d.y), slab_rcp_lean(d.z));
+    const V3 oi = o * id;
+    const GroupRec G = groups[0];
+    if (STATS) n_tests += G.n_rect[0] + G.n_rect[1] + G.n_rect[2] + G.n_flat_extra;
+    RectP r = rects + __float_as_int(G.lo.w);
+    rect_group<0>(r, G.n_rect[0], o, d, id, oi, prev, b);
+    r += G.n_rect[0];
+    rect_group<1>(r, G.n_rect[1], o, d, id, oi, prev, b);
+    r += G.n_rect[1];
+    rect_group<2>(r, G.n_rect[2], o, d, id, oi, prev, b);
+    for (int j = G.frame_first + G.n_frames; j < G.frame_first + G.n_frames + G.n_boxes; j++) {
+        const BoxRec B = boxes[j];
+        hit_box<false>(B, o, d, id, oi, prev, b);
+    }
 }
 
 // One leaf step of the BVH kernels: RT_SPEC_PRIMS primitives of the pending leaf pend, their
@@ -1435,7 +1460,11 @@ __global__ void __launch_bounds__(256, WIDTH == 4 ? RT_BVH_WAVES : RT_BVH2_WAVES
         if (!waiting && !busy) break;
         if (!busy || __popcll(waiting) >= p.refill) {
             wave_rays += (unsigned)__popcll(__ballot(done)); // one Scene.RayTrace per finished query
-            if (done) { // the query finished: planes (outside the BVH), then one bounce
+            if (done) { // the query finished: the outer records and planes (outside the BVH), then one bounce
+                // (a NaN direction, from a vertex-normal triangle, meets nothing: see path_body)
+                if (s.n_groups > 0 && !(VN && __builtin_isnan(S.d.x + S.d.y + S.d.z)))
+                    test_outer<STATS>((const RT_AS_CONST GroupRec*)pq->groups, (const RT_AS_CONST RectRec*)pq->rects,
+                                      (const RT_AS_CONST BoxRec*)pq->frames, S.o, S.d, S.prev, b, cnt.outer);
                 for (int i = s.n_bvh; i < s.n_bvh + s.n_pln; i++) {
                     const TestRec tr = tests[i];
                     hit_plane<true>(tr, i, S.o, S.d, S.prev, b);
@@ -1686,6 +1715,9 @@ __global__ void __launch_bounds__(256, WAVES) trace_rays_kernel(TraceRaysParams 
             }
             if (!more && pend < 0) {
                 trav = false;
+                if (p.outer)
+                    test_outer<false>((const RT_AS_CONST GroupRec*)p.outer, (const RT_AS_CONST RectRec*)p.outer_rects,
+                                      (const RT_AS_CONST BoxRec*)p.outer_boxes, o, d, prev, b, n_tri);
                 p.hits[idx] = make_float2(b.t, __int_as_float(b.sg));
             }
         }
@@ -1980,16 +2012,16 @@ void fill_launch(const DevScene& s, int variant, PathParams& p)
         }
     }
     const bool grouped = kernel == 1, bvh = kernel >= 2;
-    ps.n_groups = grouped ? s.n_groups_gr : 1;
+    ps.n_groups = grouped ? s.n_groups_gr : bvh ? s.n_outer : 1;
     ps.n_bvh = bvh ? s.pln0_bvh : grouped ? s.pln0_gr : s.pln0_bf;
     ps.n_slots = ps.n_bvh + s.n_pln;
     p.scene = ps;
     p.tests = bvh ? s.tests_bvh : grouped ? s.tests_gr : s.tests_bf;
     p.rows = bvh ? s.rows_bvh : nullptr;
-    p.rects = grouped ? s.rects_gr : s.rects_bf;
-    p.frames = grouped ? s.frames_gr : s.frames_bf;
+    p.rects = bvh ? s.rects_bvh : grouped ? s.rects_gr : s.rects_bf;
+    p.frames = bvh ? s.frames_bvh : grouped ? s.frames_gr : s.frames_bf;
     p.prims = bvh ? s.prims_bvh : grouped ? s.prims_gr : s.prims_bf;
-    p.groups = grouped ? s.groups_gr : s.groups_bf;
+    p.groups = bvh ? s.groups_bvh : grouped ? s.groups_gr : s.groups_bf;
     p.nodes = s.nodes;
     p.nodes4 = s.nodes4;
     p.xf = s.xf;

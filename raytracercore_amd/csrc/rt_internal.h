@@ -181,7 +181,7 @@ struct PathScene {
     int32_t n_xf;                // XformF records
     int32_t n_vn;                // triangles with vertex normals (Triangle.HasNormals); 0 removes their path
     uint32_t facts;              // FACT_* of the scene
-    int32_t n_groups;            // brute force: GroupRec records
+    int32_t n_groups;            // brute force: GroupRec records; BVH kernels: outer groups (0 or 1)
     int32_t root;                // child reference of the BVH root
     const Node4Q* hot4;          // wide kernel: the top nodes, staged in LDS (child refs | RT_HOT_BIT)
     int32_t n_hot4;
@@ -330,6 +330,12 @@ struct DevScene {
     const TestRec* tests_bvh;
     const float4* rows_bvh;     // the BVH order's TestRecs without the meta row (3 float4 per slot): compact leaves
     const PrimF* prims_bvh;
+    // outer records of the BVH order (host builder, large scenes): one GroupRec of world rects and
+    // closed boxes left out of the tree, tested when a query ends; n_outer = 0 or 1 groups
+    const RectRec* rects_bvh;
+    const FrameRec* frames_bvh;
+    const GroupRec* groups_bvh;
+    int32_t n_outer;
     const NodeF* nodes;
     int32_t n_nodes;
     int32_t root;               // child reference of the root (may be a leaf)

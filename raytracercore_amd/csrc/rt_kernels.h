@@ -78,6 +78,9 @@ struct TraceRaysParams {
     const XformF* xf;
     int root4;
     int spec;                   // blocked lanes that trigger a leaf step (as PathParams.spec)
+    const GroupRec* outer;      // the BVH order's outer group (DevScene::groups_bvh) or null
+    const RectRec* outer_rects;
+    const FrameRec* outer_boxes;
     unsigned long long* stats;  // optional [3]: node visits, leaf-step lane slots, lane slots in all
 };
 

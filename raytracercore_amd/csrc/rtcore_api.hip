@@ -145,6 +145,12 @@ struct rt_scene {
         float gpu_ms = 0.0f;
     } bvh;
     DevBuf<int32_t> order_d;      // GPU builder: primitive IDs in leaf order, planes appended
+    // Outer records (host builder, large scenes): the axis-aligned rectangles left out of the tree
+    // and tested as one brute-force group (world rects and closed boxes) when a query ends
+    std::vector<char> bvh_outer;  // per primitive: 1 = outside the tree (empty: none)
+    DevBuf<RectRec> rects_bvh;
+    DevBuf<FrameRec> frames_bvh;  // the group's BoxRecs
+    DevBuf<GroupRec> groups_bvh;
     double ms_prepare = 0, ms_bvh = 0, ms_upload = 0;
     struct { // the flat brute-force order's decomposition (build statistics)
         int rects = 0, boxes = 0, frames = 0, frame_boxes = 0, frame_rects = 0, tris = 0, sphs = 0;
@@ -232,6 +238,7 @@ struct rt_scene {
     std::array<hipEvent_t, kParamRing> slot_ev{};
     unsigned params_next = 0;
     bool has_camera = false;
+    bool flat_overflow = false; // the flat brute-force order exceeds GroupRec's counts (BruteOrder::overflow)
     hipStream_t stream = nullptr;
     // Timing of the path kernels: the i-th launch records the event pair i % kTimeRing, so a caller
     // can queue up to that many launches before it reads their durations (rt_kernel_times).
@@ -337,33 +344,44 @@ struct BruteOrder {
     std::vector<FrameRec> frames; // FrameRecs and BoxRecs
     std::vector<GroupRec> groups;
     int nr[3] = {0, 0, 0}, nt = 0, ns = 0;
+    // a group with more triangles or spheres than GroupRec::n_tri_sph holds (16 and 15 bits): the
+    // brute-force kernels cannot run the order (rt_scene_set_traversal refuses them)
+    bool overflow = false;
+    int tris0 = 0, sphs0 = 0; // triangles and spheres of the first group (the flat order's only one)
 };
 struct BruteOrders {
     BruteOrder flat, grouped;
+    BruteOrder outer; // the BVH's outer records: one group, slots numbered from 0 (planes appended)
     int nr[3] = {0, 0, 0}, nt = 0, ns = 0, np = 0;
     int group_max = 0; // primitives per group of the grouped order (kGroupMax at creation)
     BruteLayout layout;
 };
-BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<int>& xf_index, const SahBvh& sah)
+// An axis-aligned rectangle: a Mirror parallelogram with both edges on coordinate axes; returns
+// the axis of its plane, or -1.
+int rect_axis_of(const HostPrim& p)
+{
+    if (p.kind != RT_PRIM_TRIANGLE || !(p.flags & F_MIRROR) || (p.flags & F_HASNORMALS)) return -1;
+    const double e1[3] = {p.e01.x, p.e01.y, p.e01.z}, e2[3] = {p.e02.x, p.e02.y, p.e02.z};
+    for (int k = 0; k < 3; k++) {
+        const int a = (k + 1) % 3, b = (k + 2) % 3;
+        if (e1[k] != 0 || e2[k] != 0) continue;
+        const bool e1a = e1[a] != 0 && e1[b] == 0, e1b = e1[b] != 0 && e1[a] == 0;
+        const bool e2a = e2[a] != 0 && e2[b] == 0, e2b = e2[b] != 0 && e2[a] == 0;
+        if ((e1a && e2b) || (e1b && e2a)) return k;
+    }
+    return -1;
+}
+
+// outer: the primitives the BVH leaves out (rt_scene::bvh_outer, may be empty); they get an order
+// of their own (BruteOrders::outer), one group of world rects and closed boxes.
+BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<int>& xf_index, const SahBvh& sah,
+                              const std::vector<char>& outer = {})
 {
     BruteOrders out;
     const int n = (int)H.size();
     auto primf = [&](int i) { return make_primf(H, xf_index, i); };
     auto testrec = [&](int i) { return make_testrec(H, xf_index, i); };
-    // An axis-aligned rectangle: a Mirror parallelogram with both edges on coordinate axes.
-    auto rect_axis = [&](int i) {
-        const HostPrim& p = H[i];
-        if (p.kind != RT_PRIM_TRIANGLE || !(p.flags & F_MIRROR) || (p.flags & F_HASNORMALS)) return -1;
-        const double e1[3] = {p.e01.x, p.e01.y, p.e01.z}, e2[3] = {p.e02.x, p.e02.y, p.e02.z};
-        for (int k = 0; k < 3; k++) {
-            const int a = (k + 1) % 3, b = (k + 2) % 3;
-            if (e1[k] != 0 || e2[k] != 0) continue;
-            const bool e1a = e1[a] != 0 && e1[b] == 0, e1b = e1[b] != 0 && e1[a] == 0;
-            const bool e2a = e2[a] != 0 && e2[b] == 0, e2b = e2[b] != 0 && e2[a] == 0;
-            if ((e1a && e2b) || (e1b && e2a)) return k;
-        }
-        return -1;
-    };
+    auto rect_axis = [&](int i) { return rect_axis_of(H[i]); };
     auto rectrec = [&](int i, int k) {
         const HostPrim& p = H[i];
         const double v0[3] = {p.v[0].x, p.v[0].y, p.v[0].z}, e1[3] = {p.e01.x, p.e01.y, p.e01.z},
@@ -769,6 +787,11 @@ BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<
             G.hi = make_float4(hi[0], hi[1], hi[2], as_f(tri_slot));
             for (int k = 0; k < 3; k++) G.n_rect[k] = cnt[k];
             G.n_tri_sph = cnt[3] | (cnt[4] << 16);
+            if (cnt[3] > 0xFFFF || cnt[4] > 0x7FFF) o.overflow = true;
+            if (gi == 0) {
+                o.tris0 = cnt[3];
+                o.sphs0 = cnt[4];
+            }
             o.groups.push_back(G);
         }
         for (int i = 0; i < n; i++) // planes follow
@@ -785,6 +808,12 @@ BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<
     for (int i = 0; i < n; i++)
         if (kind_of[i] != 5) all.push_back(i);
     BruteOrder flat = build_order({all}, {0});
+    if (!outer.empty()) {
+        std::vector<int> ids;
+        for (int i = 0; i < n; i++)
+            if (outer[i]) ids.push_back(i);
+        out.outer = build_order({ids}, {0});
+    }
     int nr[3] = {flat.nr[0], flat.nr[1], flat.nr[2]}, nt = flat.nt, ns = flat.ns, np = 0;
     if (!flat.groups.empty()) {
         const GroupRec& G = flat.groups[0];
@@ -798,8 +827,8 @@ BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<
             out.layout.frame_boxes += F.box >= 0;
             out.layout.frame_rects += F.n_rect[0] + F.n_rect[1] + F.n_rect[2];
         }
-        out.layout.tris = G.n_tri_sph & 0xFFFF;
-        out.layout.sphs = G.n_tri_sph >> 16;
+        out.layout.tris = flat.tris0;
+        out.layout.sphs = flat.sphs0;
     }
     for (int i = 0; i < n; i++) np += kind_of[i] == 5;
     // groups: subtrees of the SAH BVH with at most kGroupMax primitives (small scenes only)
@@ -1081,9 +1110,10 @@ int upload_scene(rt_scene* s)
     // --- fast fp32 set
     auto primf = [&](int i) { return make_primf(H, xf_index, i); };
     auto testrec = [&](int i) { return make_testrec(H, xf_index, i); };
-    BruteOrders orders = make_brute_orders(H, xf_index, s->sah);
+    BruteOrders orders = make_brute_orders(H, xf_index, s->sah, s->bvh_outer);
     BruteOrder& flat = orders.flat;
     BruteOrder& grouped = orders.grouped;
+    s->flat_overflow = flat.overflow;
     int nr[3] = {orders.nr[0], orders.nr[1], orders.nr[2]}, nt = orders.nt, ns = orders.ns, np = orders.np;
     {
         const BruteLayout& L = orders.layout;
@@ -1147,6 +1177,21 @@ int upload_scene(rt_scene* s)
             bv.push_back(primf(i));
             tbv.push_back(testrec(i));
         }
+        // the outer records' slots follow the tree's (their records renumbered past it)
+        BruteOrder& ob = orders.outer;
+        if (!ob.groups.empty()) {
+            const int base = (int)bv.size(), n_slots = (int)ob.prims.size() - np;
+            bv.insert(bv.end(), ob.prims.begin(), ob.prims.begin() + n_slots);
+            tbv.insert(tbv.end(), ob.tests.begin(), ob.tests.begin() + n_slots);
+            for (RectRec& r : ob.rects) r.sg += base << 1;
+            const GroupRec& G = ob.groups[0];
+            for (int j = G.frame_first + G.n_frames; j < G.frame_first + G.n_frames + G.n_boxes; j++) {
+                BoxRec B;
+                std::memcpy(&B, &ob.frames[j], sizeof B);
+                B.sg0 += base << 1;
+                std::memcpy(&ob.frames[j], &B, sizeof B);
+            }
+        }
         for (int i = 0; i < n; i++) // planes follow the BVH's primitives in both orders
             if (H[i].kind == RT_PRIM_PLANE) {
                 bv.push_back(primf(i));
@@ -1177,6 +1222,11 @@ int upload_scene(rt_scene* s)
         HIP_TRY(s->tests_bvh.upload(tbv));
         HIP_TRY(s->nodes.upload(s->sah.nodes));
         HIP_TRY(s->nodes4.upload(s->bvh4.nodes));
+        if (!orders.outer.groups.empty()) {
+            HIP_TRY(s->rects_bvh.upload(orders.outer.rects));
+            HIP_TRY(s->frames_bvh.upload(orders.outer.frames));
+            HIP_TRY(s->groups_bvh.upload(orders.outer.groups));
+        }
     }
     HIP_TRY(s->xf.upload(xf));
     HIP_TRY(s->mats.upload(mats));
@@ -1273,7 +1323,11 @@ int upload_scene(rt_scene* s)
     // slots before the planes, per order (open boxes add placeholder slots to the brute orders)
     d.pln0_bf = (int)flat.prims.size() - np;
     d.pln0_gr = grouped.prims.empty() ? 0 : (int)grouped.prims.size() - np;
-    d.pln0_bvh = n - np;
+    d.pln0_bvh = (int)n_bvh_records - np;
+    d.rects_bvh = s->rects_bvh.p;
+    d.frames_bvh = s->frames_bvh.p;
+    d.groups_bvh = s->groups_bvh.p;
+    d.n_outer = orders.outer.groups.empty() ? 0 : 1;
     for (int k = 0; k < 3; k++) d.n_rect[k] = nr[k];
     d.n_tri = nt;
     d.n_sph = ns;
@@ -1333,6 +1387,10 @@ int resolve_traversal(rt_scene* s)
     if (s->traversal == RT_TRAVERSAL_AUTO && t == RT_TRAVERSAL_BRUTE && s->grouped_measured > 1.25)
         t = RT_TRAVERSAL_GROUPED;
     if (t == RT_TRAVERSAL_GROUPED && s->dev.n_groups_gr == 0) t = RT_TRAVERSAL_BRUTE; // too big to group
+    if (t == RT_TRAVERSAL_BRUTE && s->flat_overflow) {
+        set_error("brute-force traversal: more than 65535 triangles or 32767 spheres in the flat order");
+        return RT_ERR_ARG;
+    }
     // kernel: 0 brute force, 1 grouped brute force, 2 BVH2 (24 + kStackOverflow stack entries),
     // 3 wide BVH (RT_WIDE_STACK + kStackOverflow)
     int kernel = t == RT_TRAVERSAL_GROUPED ? 1 : 0;
@@ -1482,13 +1540,14 @@ PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint6
     if (const char* e = getenv("RTCORE_POOL_MUL")) pool_mul = std::max(1, std::min(64, atoi(e)));
     p.pool = 64;
     while (p.pool < 64 * pool_mul && p.pool < 64 * p.n_chunks) p.pool *= 2;
-    // BVH kernels: the shading phase runs once 24 lanes wait (C4 with speculative traversal:
-    // 8 / 16 / 20 / 24 / 28 / 32 lanes: 71.8 / 64.3 / 63.2 / 62.1-62.6 / 62.9 / 63.6 ms); a leaf step
-    // once 16 lanes are blocked on a pending leaf (12 / 16 / 20 / 24 / 32 / 48: 64.8 / 64.3 / 63.6 /
-    // 65.3 / 68.1 / 89.5 ms at refill 16)
-    p.refill = 24;
+    // BVH kernels: the shading phase runs once 28 lanes wait; a leaf step once 12 lanes are blocked
+    // on a pending leaf.  Round 5, C4 with the walls as outer records (profiles/r05/c4_outer_sweep.log):
+    // refill 24 / 28 / 32 at spec 16: 44.0 / 43.6 / 43.6 ms; spec 12 / 16 / 20 at refill 24: 43.8 /
+    // 44.0 / 44.5; refill 28 + spec 12 (+ leaves of <= 2): 43.2 (43.0).  Earlier tree (round 2):
+    // refill 8 / 16 / 20 / 24 / 28 / 32: 71.8 / 64.3 / 63.2 / 62.1-62.6 / 62.9 / 63.6 ms.
+    p.refill = 28;
     if (const char* e = getenv("RTCORE_BVH_REFILL")) p.refill = std::max(1, std::min(64, atoi(e)));
-    p.spec = 16;
+    p.spec = 12;
     if (const char* e = getenv("RTCORE_BVH_SPEC")) p.spec = std::max(1, std::min(64, atoi(e)));
     // XCD-local item ranges: the 8x8 blocks cut into kMaxSplit runs of consecutive blocks (horizontal
     // strips of the tile), each dealt first to the workgroups of one XCD, so that one XCD's waves work
@@ -1808,9 +1867,26 @@ int build_bvhs(rt_scene* s)
         set_error("rt_scene_create: more than 2^27 - " + std::to_string(kTestSpares) + " BVH primitives");
         return RT_ERR_ARG;
     }
-    int max_leaf = n > 256 ? 3 : 2; // C4 mesh: leaves of <= 2, 3, 4, 6, 8 -> 70.6, 70.5, 72.2, 76.1, 80.2 ms
-    if (const char* e = getenv("RTCORE_MAX_LEAF")) max_leaf = std::max(1, std::min(8, atoi(e))); // tuning
     s->bvh.builder = builder_for(nb);
+    // Outer records: in a large scene (nb > 4096: no grouped brute-force order, which would cut
+    // this tree) the axis-aligned rectangles -- a room's walls, a light box -- stay out of the
+    // tree and are tested as one group of rects and closed boxes when a query ends.  Their
+    // large boxes overlap the whole scene near the root (tools/bvh_sim.cpp on C4's mesh: node
+    // visits per query 8.75 -> 7.88, primitive tests 5.33 -> 2.46; measured: C4 46.5 -> 44.0 ms,
+    // nodes 9.16 -> 8.34 and leaf tests 5.75 -> 2.88 per ray segment).  RTCORE_BVH_OUTER=0: off.
+    bool outer_on = nb > 4096 && s->bvh.builder == RT_BVH_BUILDER_HOST;
+    if (const char* e = getenv("RTCORE_BVH_OUTER")) outer_on = outer_on && atoi(e) != 0;
+    s->bvh_outer.clear();
+    if (outer_on) {
+        std::vector<char> m(n, 0);
+        int k = 0;
+        for (int i = 0; i < n; i++) k += (m[i] = rect_axis_of(H[i]) >= 0);
+        if (k > 0 && k < nb) s->bvh_outer = std::move(m);
+    }
+    // leaves of <= 3 primitives, <= 2 with outer records (C4, round 2: leaves of <= 2, 3, 4, 6, 8 ->
+    // 70.6, 70.5, 72.2, 76.1, 80.2 ms; round 5 with outer records: 2 / 3 / 4 -> 43.8 / 44.0 / 47.2)
+    int max_leaf = n > 256 && s->bvh_outer.empty() ? 3 : 2;
+    if (const char* e = getenv("RTCORE_MAX_LEAF")) max_leaf = std::max(1, std::min(8, atoi(e))); // tuning
     if (s->bvh.builder == RT_BVH_BUILDER_HOST) {
         // the wide tree: greedy collapse of the BVH2 (default), or the SAH-optimal collapse of the
         // whole SAH tree (RTCORE_WIDE_COLLAPSE=1; RTCORE_WIDE_CNODE / _CPRIM / _LEAF set its costs)
@@ -1820,7 +1896,7 @@ int build_bvhs(rt_scene* s)
         if (const char* e = getenv("RTCORE_WIDE_CNODE")) wc.c_node = (float)atof(e);
         if (const char* e = getenv("RTCORE_WIDE_CPRIM")) wc.c_prim = (float)atof(e);
         if (const char* e = getenv("RTCORE_WIDE_LEAF")) wc.max_leaf = std::max(1, std::min(8, atoi(e)));
-        s->sah = build_sah_bvh(H, max_leaf, sah_collapse);
+        s->sah = build_sah_bvh(H, max_leaf, sah_collapse, s->bvh_outer.empty() ? nullptr : &s->bvh_outer);
         s->bvh4 = build_bvh4(s->sah, sah_collapse ? &wc : nullptr);
         s->sah.full.clear(); // only the collapse reads the whole tree
         s->sah.full.shrink_to_fit();
@@ -2078,6 +2154,11 @@ int rt_debug_trace_rays(rt_scene* s, const void* d_rays, uint32_t n, void* d_hit
     p.nodes4 = s->dev.nodes4;
     p.xf = s->dev.xf;
     p.root4 = s->dev.root4;
+    if (s->dev.n_outer > 0) {
+        p.outer = s->dev.groups_bvh;
+        p.outer_rects = s->dev.rects_bvh;
+        p.outer_boxes = s->dev.frames_bvh;
+    }
     p.spec = 16;
     if (const char* e = getenv("RTCORE_BVH_SPEC")) p.spec = std::max(1, std::min(64, atoi(e)));
     p.stats = static_cast<unsigned long long*>(d_stats);
@@ -2147,7 +2228,8 @@ int rt_scene_get_build_stats(const rt_scene* s, double* out, int32_t n)
                                            (double)L.frame_rects, (double)L.tris, (double)L.sphs,
                                            (double)s->dev.n_hot4, (double)s->jit.status, s->jit.compile_ms,
                                            s->jit.from_cache ? 1.0 : 0.0, (double)L.group_max,
-                                           (double)s->bvh.leaves4, (double)s->bvh.compact4};
+                                           (double)s->bvh.leaves4, (double)s->bvh.compact4,
+                                           (double)std::count(s->bvh_outer.begin(), s->bvh_outer.end(), 1)};
     for (int i = 0; i < n && i < RT_BUILD_STATS_COUNT; i++) out[i] = v[i];
     return RT_OK;
 }
@@ -2165,8 +2247,10 @@ int rt_scene_check_bvh(rt_scene* s)
     HIP_TRY(hipSetDevice(s->device));
     const auto& H = s->host;
     const int n = (int)H.size();
+    // nb: the slots the tree's leaves address (outer records, when present, follow them)
+    auto outside = [&](int i) { return H[i].kind == RT_PRIM_PLANE || (!s->bvh_outer.empty() && s->bvh_outer[i]); };
     int nb = 0;
-    for (const HostPrim& p : H) nb += p.kind != RT_PRIM_PLANE;
+    for (int i = 0; i < n; i++) nb += !outside(i);
     std::vector<NodeF> n2(s->bvh.n_nodes2);
     std::vector<Node4Q> n4(s->bvh.n_nodes4);
     std::vector<PrimF> recs(nb);
@@ -2220,7 +2304,7 @@ int rt_scene_check_bvh(rt_scene* s)
         }
         for (int k = first; k < first + cnt; k++) {
             const int p = id[k];
-            if (p < 0 || p >= n || H[p].kind == RT_PRIM_PLANE) {
+            if (p < 0 || p >= n || outside(p)) {
                 err = "leaf record with a bad primitive ID";
                 return;
             }
@@ -2266,7 +2350,7 @@ int rt_scene_check_bvh(rt_scene* s)
     };
     if (nb > 0) walk2(s->bvh.root2, 0);
     for (int i = 0; i < n && err.empty(); i++)
-        if (seen[i] != (H[i].kind == RT_PRIM_PLANE ? 0 : 1))
+        if (seen[i] != (outside(i) ? 0 : 1))
             err = "BVH2: primitive " + std::to_string(i) + " referenced " + std::to_string(seen[i]) + " times";
     if (err.empty() && max_depth > s->bvh.depth2) err = "BVH2 deeper than its recorded depth";
     // wide tree
@@ -2319,7 +2403,7 @@ int rt_scene_check_bvh(rt_scene* s)
     };
     if (err.empty() && nb > 0) walk4(s->bvh.root4, 0);
     for (int i = 0; i < n && err.empty(); i++)
-        if (seen[i] != (H[i].kind == RT_PRIM_PLANE ? 0 : 1))
+        if (seen[i] != (outside(i) ? 0 : 1))
             err = "wide tree: primitive " + std::to_string(i) + " referenced " + std::to_string(seen[i]) + " times";
     if (err.empty() && max_stack > s->bvh.stack4) err = "wide tree needs more stack than recorded";
     if (!err.empty()) {
@@ -2440,9 +2524,14 @@ int rt_scene_set_traversal(rt_scene* s, int32_t traversal)
         return RT_ERR_ARG;
     }
     HIP_TRY(hipSetDevice(s->device));
+    const int before = s->traversal;
     s->traversal = traversal;
     const int rc = (traversal == RT_TRAVERSAL_AUTO && s->has_camera) ? calibrate_grouping(s) : resolve_traversal(s);
-    if (rc == RT_OK && s->has_camera) (void)prepare_jit(s);
+    if (rc != RT_OK) {
+        s->traversal = before; // a refused mode leaves the scene as it was
+        return rc;
+    }
+    if (s->has_camera) (void)prepare_jit(s);
     return rc;
 }
 

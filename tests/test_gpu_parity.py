@@ -67,6 +67,15 @@ def test_mesh_primary_ids_bitexact(rc):
     assert (ids >= 11).mean() > 0.02  # the height field (IDs after the room and light box) is in view
     counts = gpu.bvh_counts(40, 20, 24, 16)
     assert np.array_equal(counts, _oracle(rc, scene, size).bvh_counts(40, 20, 24, 16))
+    # the room's and light box's 11 rectangles are outer records; the tree holds the 1M triangles
+    bs = gpu.build_stats()
+    assert bs["outer_prims"] == 11 and bs["flat_tris"] == 1000000 and bs["flat_boxes"] == 2
+    gpu.check_bvh()
+    # 1M triangles do not fit the brute-force group's 16-bit count: refused, the BVH mode kept
+    with pytest.raises(rc.RtError):
+        gpu.set_traversal(rc.RT_TRAVERSAL_BRUTE)
+    assert gpu.info().traversal == rc.RT_TRAVERSAL_BVH
+    gpu.close()
 
 
 @pytest.mark.parametrize("name", ["bounce.txt", "die.txt"])
@@ -993,17 +1002,20 @@ def test_scene_specialised_cache_untrusted_dir_is_not_used(tmp_path):
     assert _cache_probe(fresh, 3)["cached"] == 1.0
 
 
-def test_trace_only_kernel_reproduces_logged_hits(rc):
+@pytest.mark.parametrize("nx", [41, 71])
+def test_trace_only_kernel_reproduces_logged_hits(rc, nx):
     """rt_debug_ray_log + rt_debug_trace_rays (the wavefront-split measurement): the
     instrumented wide-BVH kernel logs every finished query of a small mesh render, and the
-    trace-only kernel re-traces them at 6, 7 and 8 waves per SIMD with bit-identical closest hits."""
+    trace-only kernel re-traces them at 6, 7 and 8 waves per SIMD with bit-identical closest hits.
+    nx = 71 (5.7k BVH primitives) has the room's walls as outer records, nx = 41 in the tree."""
     import torch
 
     from raytracercore_amd.scenes import mesh_scene_text
 
     W, H, spp = 96, 64, 4
-    scene = rc.SceneLoader.from_text(mesh_scene_text(nx=41, ny=41))
+    scene = rc.SceneLoader.from_text(mesh_scene_text(nx=nx, ny=41))
     gpu = rc.GpuRaytracer(scene, 0, size=(W, H), traversal=rc.RT_TRAVERSAL_BVH)
+    assert (gpu.build_stats()["outer_prims"] > 0) == (nx == 71)
     dev = torch.device("cuda", 0)
     cap = W * H * spp * 12
     log = torch.zeros(cap * 12, dtype=torch.float32, device=dev)
