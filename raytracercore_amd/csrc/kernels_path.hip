@@ -1461,10 +1461,12 @@ __global__ void __launch_bounds__(256, WIDTH == 4 ? RT_BVH_WAVES : RT_BVH2_WAVES
         if (!busy || __popcll(waiting) >= p.refill) {
             wave_rays += (unsigned)__popcll(__ballot(done)); // one Scene.RayTrace per finished query
             if (done) { // the query finished: the outer records and planes (outside the BVH), then one bounce
+#if !RT_OUTER_AT_START
                 // (a NaN direction, from a vertex-normal triangle, meets nothing: see path_body)
                 if (s.n_groups > 0 && !(VN && __builtin_isnan(S.d.x + S.d.y + S.d.z)))
                     test_outer<STATS>((const RT_AS_CONST GroupRec*)pq->groups, (const RT_AS_CONST RectRec*)pq->rects,
                                       (const RT_AS_CONST BoxRec*)pq->frames, S.o, S.d, S.prev, b, cnt.outer);
+#endif
                 for (int i = s.n_bvh; i < s.n_bvh + s.n_pln; i++) {
                     const TestRec tr = tests[i];
                     hit_plane<true>(tr, i, S.o, S.d, S.prev, b);
@@ -1493,6 +1495,11 @@ __global__ void __launch_bounds__(256, WIDTH == 4 ? RT_BVH_WAVES : RT_BVH2_WAVES
                     more = false;
                 }
                 b = query_start<VN>(s, S.prev);
+#if RT_OUTER_AT_START
+                if (s.n_groups > 0 && !(VN && __builtin_isnan(S.d.x + S.d.y + S.d.z)))
+                    test_outer<STATS>((const RT_AS_CONST GroupRec*)pq->groups, (const RT_AS_CONST RectRec*)pq->rects,
+                                      (const RT_AS_CONST BoxRec*)pq->frames, S.o, S.d, S.prev, b, cnt.outer);
+#endif
                 trav = true;
             }
         }

@@ -281,16 +281,18 @@ def test_traversal_modes_agree(rc, scenes, name, mode):
     assert np.allclose(sa, sb, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("mode", ["BVH", "BVH2", "GROUPED"])
-def test_traversal_modes_agree_mesh(rc, mode):
-    """The same on a small procedural height field (3,200 triangles): BVH == brute force up to
-    ties on shared triangle edges."""
+@pytest.mark.parametrize("mode,nx", [("BVH", 41), ("BVH2", 41), ("GROUPED", 41), ("BVH", 71), ("BVH2", 71)])
+def test_traversal_modes_agree_mesh(rc, mode, nx):
+    """The same on a small procedural height field (3,200 triangles; 5,600 at nx = 71, where the
+    BVH kernels test the room and the light box as outer records): BVH == brute force up to ties
+    on shared triangle edges."""
     from raytracercore_amd.scenes import mesh_scene_text
 
-    scene = rc.SceneLoader.from_text(mesh_scene_text(nx=41, ny=41))
+    scene = rc.SceneLoader.from_text(mesh_scene_text(nx=nx, ny=41))
     a = rc.GpuRaytracer(scene, 0, size=(96, 64), traversal=rc.RT_TRAVERSAL_BRUTE)
     b = rc.GpuRaytracer(scene, 0, size=(96, 64), traversal=getattr(rc, "RT_TRAVERSAL_" + mode))
     assert b.info().traversal == getattr(rc, "RT_TRAVERSAL_" + mode)
+    assert (b.build_stats()["outer_prims"] == 11) == (nx == 71)
     sa, na, ma, ra = a.render_tile(0, 0, 96, 64, 16, seed=4)
     sb, nb, mb, rb = b.render_tile(0, 0, 96, 64, 16, seed=4)
     assert abs(int(ma.sum()) - int(mb.sum())) <= 2
