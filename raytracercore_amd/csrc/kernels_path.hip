@@ -1041,6 +1041,9 @@ __device__ __forceinline__ void lane_init(Lane& L)
 // NT: store the item partials non-temporally (the BVH kernels: their 16-B-per-sample partial
 // stream would otherwise push the scene out of the Infinity Cache; C4 52.74-52.86 -> 52.30-52.37
 // ms; the brute-force kernels keep normal stores, die.txt C3 27.5 -> 27.7-27.8 ms with them)
+#ifndef RT_PKEY_AT_START
+#define RT_PKEY_AT_START 0 // NT (BVH) kernels: derive the pixel key at each sample start instead of holding it
+#endif
 template <bool NT, class ParT, class SceneT, class CamT>
 __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const SceneT& s, const CamT& cam, int lane,
                                       unsigned total)
@@ -1124,7 +1127,7 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
                     // the brute-force kernels read the key from the scene's table (the same value:
                     // two hash rounds fewer per item open, which runs in most iterations)
                     if (!NT && p.pkeys) L.pkey = p.pkeys[px];
-                    else L.pkey = rt_rng_pixel_key(p.seed_key, px);
+                    else if (!(NT && RT_PKEY_AT_START)) L.pkey = rt_rng_pixel_key(p.seed_key, px);
                 }
             }
         }
@@ -1136,6 +1139,9 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
         }
     }
     if (L.active && L.item_open && !L.live && L.cnt >= 65536u) {
+        if (NT && RT_PKEY_AT_START) // the key from the pixel at every sample start: two registers fewer held
+            L.pkey = rt_rng_pixel_key(p.seed_key, (unsigned long long)L.fy * (unsigned long long)p.scene.width +
+                                                      (unsigned long long)L.fx);
         S.rng = rt_rng_from_pixel_key(L.pkey, p.sample_base + (unsigned long long)L.s_next);
         start_sample<!NT>(cam, L.fx, L.fy, S);
         L.live = true;
