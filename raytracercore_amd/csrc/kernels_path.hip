@@ -1041,6 +1041,31 @@ __device__ __forceinline__ void lane_init(Lane& L)
 // NT: store the item partials non-temporally (the BVH kernels: their 16-B-per-sample partial
 // stream would otherwise push the scene out of the Infinity Cache; C4 52.74-52.86 -> 52.30-52.37
 // ms; the brute-force kernels keep normal stores, die.txt C3 27.5 -> 27.7-27.8 ms with them)
+#ifndef RT_MBCNT
+#define RT_MBCNT 0 // NT (BVH) kernels: a lane's rank among the set lanes of m by v_mbcnt (no lane mask held)
+#endif
+// the set bits of the wave mask m below this lane (v_mbcnt_lo / _hi: no 64-bit lane mask register,
+// which the compiler hoists out of the loop and then spills)
+__device__ __forceinline__ unsigned lanes_below(unsigned long long m)
+{
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+#ifndef RT_PACK_XY
+#define RT_PACK_XY 0 // NT (BVH) kernels: the pixel's frame x and y in one register (L.fx = x | y << 16)
+#endif
+template <bool NT>
+__device__ __forceinline__ int lane_fx(const Lane& L)
+{
+    return (NT && RT_PACK_XY) ? (L.fx & 0xFFFF) : L.fx;
+}
+template <bool NT>
+__device__ __forceinline__ int lane_fy(const Lane& L)
+{
+    return (NT && RT_PACK_XY) ? (int)((unsigned)L.fx >> 16) : L.fy;
+}
+#ifndef RT_ID_AFTER_SHADE
+#define RT_ID_AFTER_SHADE 0
+#endif
 #ifndef RT_PKEY_AT_START
 #define RT_PKEY_AT_START 0 // NT (BVH) kernels: derive the pixel key at each sample start instead of holding it
 #endif
@@ -1086,7 +1111,7 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
             fresh = __builtin_amdgcn_readfirstlane(fresh);
         }
         if (need) {
-            const unsigned r = (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+            const unsigned r = (NT && RT_MBCNT) ? lanes_below(m) : (unsigned)__popcll(m & ((1ull << lane) - 1ull));
             L.item = r < avail ? L.pool_next + r : fresh + (r - avail);
             if (L.item >= total) {
                 L.active = false;
@@ -1120,10 +1145,11 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
                         }
                         L.fy = p.y0 + ((int)bq * p.band_stride + p.band_offset) * p.band + (int)br;
                     }
+                    if (NT && RT_PACK_XY) L.fx |= L.fy << 16; // one register for both (frames < 65536 wide / high)
                     // the frame width from the launch record (a scene-specialised build's constant
                     // scene leaves it out, so one build serves every frame size)
-                    const unsigned long long px =
-                        (unsigned long long)L.fy * (unsigned long long)p.scene.width + (unsigned long long)L.fx;
+                    const unsigned long long px = (unsigned long long)lane_fy<NT>(L) * (unsigned long long)p.scene.width +
+                                                  (unsigned long long)lane_fx<NT>(L);
                     // the brute-force kernels read the key from the scene's table (the same value:
                     // two hash rounds fewer per item open, which runs in most iterations)
                     if (!NT && p.pkeys) L.pkey = p.pkeys[px];
@@ -1140,10 +1166,10 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
     }
     if (L.active && L.item_open && !L.live && L.cnt >= 65536u) {
         if (NT && RT_PKEY_AT_START) // the key from the pixel at every sample start: two registers fewer held
-            L.pkey = rt_rng_pixel_key(p.seed_key, (unsigned long long)L.fy * (unsigned long long)p.scene.width +
-                                                      (unsigned long long)L.fx);
+            L.pkey = rt_rng_pixel_key(p.seed_key, (unsigned long long)lane_fy<NT>(L) * (unsigned long long)p.scene.width +
+                                                      (unsigned long long)lane_fx<NT>(L));
         S.rng = rt_rng_from_pixel_key(L.pkey, p.sample_base + (unsigned long long)L.s_next);
-        start_sample<!NT>(cam, L.fx, L.fy, S);
+        start_sample<!NT>(cam, lane_fx<NT>(L), lane_fy<NT>(L), S);
         L.live = true;
     }
 }
@@ -1482,7 +1508,8 @@ __global__ void __launch_bounds__(256, WIDTH == 4 ? RT_BVH_WAVES : RT_BVH2_WAVES
                     if (q < p.ray_log_cap) {
                         float4* r = p.ray_log + 3 * (size_t)q;
                         r[0] = make_float4(S.o.x, S.o.y, S.o.z, __int_as_float(S.prev));
-                        r[1] = make_float4(S.d.x, S.d.y, S.d.z, __int_as_float(L.fy * p.scene.width + L.fx));
+                        r[1] = make_float4(S.d.x, S.d.y, S.d.z,
+                                           __int_as_float(lane_fy<true>(L) * p.scene.width + lane_fx<true>(L)));
                         r[2] = make_float4(b.t, __int_as_float(b.sg), __int_as_float(S.bounce), 0.0f);
                     }
                 }
@@ -1491,7 +1518,7 @@ __global__ void __launch_bounds__(256, WIDTH == 4 ? RT_BVH_WAVES : RT_BVH2_WAVES
             }
             refill<true>(L, S, p, s, *cp, lane, total);
             if (L.live && !trav) { // start the next query
-                id = v3(slab_rcp(S.d.x), slab_rcp(S.d.y), slab_rcp(S.d.z));
+                if (!RT_ID_AFTER_SHADE) id = v3(slab_rcp(S.d.x), slab_rcp(S.d.y), slab_rcp(S.d.z));
                 ref = s.root;
                 sp = 0;
                 pend = -1;
@@ -1508,6 +1535,9 @@ __global__ void __launch_bounds__(256, WIDTH == 4 ? RT_BVH_WAVES : RT_BVH2_WAVES
 #endif
                 trav = true;
             }
+            // RT_ID_AFTER_SHADE: 1/d of every lane's query rebuilt after the shading phase, so that the
+            // three registers are free inside it (the traversing lanes recompute the same values)
+            if (RT_ID_AFTER_SHADE) id = v3(slab_rcp(S.d.x), slab_rcp(S.d.y), slab_rcp(S.d.z));
         }
 #if RT_BVH_SPEC
         // Speculative traversal (Aila & Laine 2009): a lane that reaches a leaf keeps it pending and
