@@ -214,6 +214,16 @@ def test_brute_layout_shipped_scenes(rc):
     assert d["groups"] > 1 and d["grouped_slots"] >= 29
 
 
+def test_brute_layout_counts_past_16_bits(rc):
+    """A flat order of 80,000 triangles: the layout reports the true count (GroupRec packs
+    triangles and spheres into 16 + 15 bits, so the brute-force kernels refuse such an order,
+    rt_scene_set_traversal; the statistic used to show the truncated 14,464)."""
+    from raytracercore_amd.scenes import mesh_scene_text
+
+    got = _layout(rc, mesh_scene_text(nx=201, ny=201))
+    assert (got["tris"], got["boxes"], got["rects"], got["spheres"]) == (80000, 2, 0, 0)
+
+
 HEAD = "size 16 12\ncamera 0 -6 1, 0 0 0, 0 0 1, 60\n"
 
 
