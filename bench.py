@@ -242,12 +242,18 @@ def frame_split(args) -> int:
     acc = (np.zeros((W, H, 3), np.float64), np.zeros((W, H), np.uint32), np.zeros((W, H), np.uint32))
     for k in range(args.warmup):
         frame.render(frame_spp, args.seed, k * frame_spp, out=acc)
+    # two-stage pipeline (rt_frame_submit / rt_frame_collect): step k+1 renders on the devices while
+    # step k is gathered, copied to the host and merged; every step is collected inside the timing
     rays = 0
     step_ms = []
+    first, last = args.warmup, args.warmup + args.steps
     t0 = time.perf_counter()
-    for k in range(args.warmup, args.warmup + args.steps):
+    frame.submit(frame_spp, args.seed, first * frame_spp)
+    for k in range(first, last):
         s0 = time.perf_counter()
-        rays += frame.render(frame_spp, args.seed, k * frame_spp, out=acc)[3]
+        if k + 1 < last:
+            frame.submit(frame_spp, args.seed, (k + 1) * frame_spp)
+        rays += frame.collect(acc)[3]
         step_ms.append((time.perf_counter() - s0) * 1e3)
     elapsed = time.perf_counter() - t0
     expect = frame_spp * (args.warmup + args.steps)
@@ -263,15 +269,37 @@ def frame_split(args) -> int:
         "data": "synthetic: the reference's own scene file (tests/golden/scenes) with seeded camera samples",
         "config": {"workload": f"{scene_file} camera {cam} {W}x{H} x {spp} spp per GPU per step",
                    "parallelism": f"rt_frame: one process, {n} GPU(s), interleaved 8-row band sets, "
-                                  + ("one ncclGather over xGMI per step" if n > 1 else "no collective")
-                                  + ", merge into host SampleSet buffers"},
+                                  + ("one ncclGather over xGMI per step" if n > 1 else "a one-rank RCCL gather")
+                                  + ", merge into host SampleSet buffers overlapped with the next step's render"},
         "step_ms_min": round(min(step_ms), 3), "step_ms_max": round(max(step_ms), 3),
         "roofline": None,
         "note": "host-buffer rate (includes the gather, the device -> host copy of 32 B per pixel and the host "
-                "merge); the HBM-resident rate of the same per-GPU work is the default split's `value`",
+                "merge, the last step's exposed); the HBM-resident rate of the same per-GPU work is the default "
+                "split's `value`",
     }
     print(json.dumps(out), flush=True)
     return 0
+
+
+def launch_ranks(args_list, n: int) -> int:
+    """`--gpus N` (N > 1) without a launcher: start N fresh rank processes of this script (one per GPU,
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run would) and return the worst
+    exit status.  Runs before anything here touches the GPU; the children are new processes, not an
+    exec of this one.  Rank 0's JSON line is the only one printed."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:  # a free port on the loopback for the rendezvous
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(args_list), env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
 
 
 def main() -> int:
@@ -290,9 +318,17 @@ def main() -> int:
                          "one rank per GPU over torch.distributed; or `frame`: ONE process drives --gpus GPUs "
                          "through the library's own rt_frame (the product path a C# host calls: band sets, "
                          "ncclGather to device 0, merge into host SampleSet buffers)")
+    ap.add_argument("--dump", default="", help="rank 0 writes the frame accumulators of the warm-up and timed "
+                                               "steps (sum, samples, misses) to this .npz (tests)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be at least 1")
     if args.split == "frame":
         return frame_split(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(sys.argv[1:], args.gpus)
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE')}: launch one rank per GPU")
 
     import numpy as np
     import torch
@@ -310,6 +346,8 @@ def main() -> int:
             dist.init_process_group(backend="gloo")
         else:
             dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"world size {dist.get_world_size()} != --gpus {args.gpus}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -442,6 +480,9 @@ def main() -> int:
         expect = expect_per_step * (args.steps + args.warmup)
         if not np.all(n_all + m_all == expect):
             raise SystemExit(f"sample bookkeeping mismatch: {np.unique(n_all + m_all)} != {expect}")
+        if args.dump:
+            np.savez(args.dump, sum=f_sum.cpu().numpy().reshape(3, H, W), samples=n_all.reshape(H, W),
+                     misses=m_all.reshape(H, W))
 
     multi = None
     if world > 1:
@@ -501,7 +542,7 @@ def main() -> int:
             "metric": metric,
             "value": round(total_rays / elapsed / 1e6, 2),
             "unit": "Mrays/s",
-            "n_gpus": world,
+            "n_gpus": dist.get_world_size() if world > 1 else 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),

@@ -38,9 +38,10 @@
 extern "C" {
 #endif
 
-#define RTCORE_ABI_VERSION 4 /* 2: rt_frame_*, rt_render_bands, sample_base in rt_render_frame_multi;
+#define RTCORE_ABI_VERSION 5 /* 2: rt_frame_*, rt_render_bands, sample_base in rt_render_frame_multi;
                                 3: rt_set_jit, rt_scene_get_jit_error, build stats [15..17];
-                                4: rt_kernel_times */
+                                4: rt_kernel_times;
+                                5: rt_frame_submit / rt_frame_collect / rt_frame_inject_fault */
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -180,6 +181,9 @@ typedef enum rt_bvh_builder {
 
 /* ---------------------------------------------------------------- library ---- */
 int rt_abi_version(void);
+/* "src-sha256=<hex> extra=<flags>": the hash of the sources the library was built from and the
+ * extra compiler flags of its build (raytracercore_amd/csrc/source_hash.py recomputes the hash). */
+const char* rt_build_info(void);
 int rt_device_count(void);
 /* Copies the calling thread's last error message (NUL-terminated); returns its length. */
 int rt_last_error(char* buf, int32_t cap);
@@ -383,6 +387,21 @@ int rt_frame_create(const rt_scene_params* params, const rt_prim* prims, int32_t
 int rt_frame_set_camera(rt_frame* frame, const rt_camera* camera);
 int rt_frame_render(rt_frame* frame, int32_t spp, uint64_t seed, uint64_t sample_base,
                     rt_color* sum_rgb, uint32_t* samples, uint32_t* misses, uint64_t* rays_out);
+/*
+ * rt_frame_render in two phases, for a host that keeps the devices busy while it merges: submit
+ * queues a render (every device's band set, the RCCL gather to device 0 and the copy of the
+ * gathered slots into pinned host memory) and returns at once; collect waits for the oldest
+ * submitted render and adds it into the caller's buffers (as rt_frame_render).  At most two
+ * renders are in flight (RT_ERR_STATE otherwise), so submit(k+1) before collect(k) overlaps
+ * render k+1 with the gather, copy and merge of render k -- FullRaytracer's update loop
+ * (FullRaytracer.cs:326-344) merging finished passes while the workers render the next.  No
+ * caller buffer is held between calls.  After an error every queued render is dropped.
+ */
+int rt_frame_submit(rt_frame* frame, int32_t spp, uint64_t seed, uint64_t sample_base);
+int rt_frame_collect(rt_frame* frame, rt_color* sum_rgb, uint32_t* samples, uint32_t* misses,
+                     uint64_t* rays_out);
+/* Test hook: point 1 makes the next gather fail inside its RCCL group (the group is still closed). */
+int rt_frame_inject_fault(rt_frame* frame, int32_t point);
 void rt_frame_destroy(rt_frame* frame);
 
 /* One-shot rt_frame_create + rt_frame_render + rt_frame_destroy. */

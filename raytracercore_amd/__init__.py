@@ -23,7 +23,7 @@ LIB_PATH = os.path.join(_HERE, "librtcore_hip.so")
 REPO_ROOT = os.path.dirname(_HERE)
 
 RT_OK = 0
-ABI_VERSION = 4  # RTCORE_ABI_VERSION of include/rtcore.h
+ABI_VERSION = 5  # RTCORE_ABI_VERSION of include/rtcore.h
 RT_PRIM_TRIANGLE, RT_PRIM_SPHERE, RT_PRIM_PLANE = 0, 1, 2
 RT_FLAG_MIRROR, RT_FLAG_TWOSIDED, RT_FLAG_INVERT, RT_FLAG_HASNORMALS, RT_FLAG_TRANSFORMED = 1, 2, 4, 8, 16
 RT_CAMERA_FRUSTUM, RT_CAMERA_ORTHO = 0, 1
@@ -121,6 +121,7 @@ def load_library(path: str = "") -> C.CDLL:
     P = C.POINTER
     sig = {
         "rt_abi_version": (C.c_int, []),
+        "rt_build_info": (C.c_char_p, []),
         "rt_device_count": (C.c_int, []),
         "rt_last_error": (C.c_int, [C.c_char_p, C.c_int32]),
         "rt_scene_create": (C.c_int, [P(rt_scene_params), P(rt_prim), C.c_int32, C.c_int32, P(C.c_void_p)]),
@@ -164,6 +165,9 @@ def load_library(path: str = "") -> C.CDLL:
         "rt_frame_set_camera": (C.c_int, [C.c_void_p, P(rt_camera)]),
         "rt_frame_render": (C.c_int, [C.c_void_p, C.c_int32, C.c_uint64, C.c_uint64, P(rt_color), P(C.c_uint32),
                                       P(C.c_uint32), P(C.c_uint64)]),
+        "rt_frame_submit": (C.c_int, [C.c_void_p, C.c_int32, C.c_uint64, C.c_uint64]),
+        "rt_frame_collect": (C.c_int, [C.c_void_p, P(rt_color), P(C.c_uint32), P(C.c_uint32), P(C.c_uint64)]),
+        "rt_frame_inject_fault": (C.c_int, [C.c_void_p, C.c_int32]),
         "rt_frame_destroy": (None, [C.c_void_p]),
         "rt_parse_scene": (C.c_int, [C.c_char_p, P(rt_scene_params), P(rt_prim), P(C.c_int32), P(rt_camera),
                                      P(C.c_int32)]),
@@ -496,12 +500,38 @@ class GpuFrame:
         W, H = self.width, self.height
         if out is None:
             out = (np.zeros((W, H, 3), np.float64), np.zeros((W, H), np.uint32), np.zeros((W, H), np.uint32))
-        s, n, m = out
+        s, n, m = self._check_out(out)
         rays = C.c_uint64(0)
         _check(self.lib.rt_frame_render(self.handle, spp, seed, sample_base, s.ctypes.data_as(C.POINTER(rt_color)),
                                         n.ctypes.data_as(C.POINTER(C.c_uint32)),
                                         m.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(rays)))
         return s, n, m, rays.value
+
+    def submit(self, spp: int, seed: int = 0, sample_base: int = 0) -> None:
+        """rt_frame_submit: queue a render (band sets, gather, host copy) and return at once."""
+        _check(self.lib.rt_frame_submit(self.handle, spp, seed, sample_base))
+
+    def collect(self, out):
+        """rt_frame_collect: wait for the oldest submitted render and add it into out = (sum[W,H,3],
+        samples[W,H], misses[W,H]); returns (sum, samples, misses, rays)."""
+        s, n, m = self._check_out(out)
+        rays = C.c_uint64(0)
+        _check(self.lib.rt_frame_collect(self.handle, s.ctypes.data_as(C.POINTER(rt_color)),
+                                         n.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                         m.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(rays)))
+        return s, n, m, rays.value
+
+    def inject_fault(self, point: int) -> None:
+        """rt_frame_inject_fault (test hook): 1 = the next gather fails inside its RCCL group."""
+        _check(self.lib.rt_frame_inject_fault(self.handle, point))
+
+    def _check_out(self, out):
+        W, H = self.width, self.height
+        s, n, m = out
+        for a, dt, shape in ((s, np.float64, (W, H, 3)), (n, np.uint32, (W, H)), (m, np.uint32, (W, H))):
+            if not (isinstance(a, np.ndarray) and a.dtype == dt and a.shape == shape and a.flags.c_contiguous):
+                raise ValueError(f"GpuFrame: outputs must be C-contiguous {np.dtype(dt).name}{shape} arrays")
+        return s, n, m
 
     def close(self) -> None:
         if self.handle:
@@ -536,6 +566,15 @@ def scatter_band_slot(slot: np.ndarray, plane: int, width: int, height: int, ban
     (sum[W,H,3], samples[W,H], misses[W,H])."""
     s, n, m = out
     slot = np.ascontiguousarray(slot, dtype=np.float64)
+    # the C side writes through raw pointers: refuse anything but the exact layouts it assumes
+    for a, dt, shape in ((s, np.float64, (width, height, 3)), (n, np.uint32, (width, height)),
+                         (m, np.uint32, (width, height))):
+        if not (isinstance(a, np.ndarray) and a.dtype == dt and a.shape == shape and a.flags.c_contiguous
+                and a.flags.writeable):
+            raise ValueError(f"scatter_band_slot: outputs must be writeable C-contiguous {np.dtype(dt).name}"
+                             f"{shape} arrays")
+    if plane < 0 or slot.size < 4 * plane:
+        raise ValueError(f"scatter_band_slot: slot holds {slot.size} float64, needs 4 * plane = {4 * plane}")
     _check(load_library().rt_scatter_band_slot(slot.ctypes.data_as(C.c_void_p), plane, width, height, band,
                                                band_stride, band_offset, s.ctypes.data_as(C.POINTER(rt_color)),
                                                n.ctypes.data_as(C.POINTER(C.c_uint32)),

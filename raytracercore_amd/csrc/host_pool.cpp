@@ -8,6 +8,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdlib>
+#include <exception>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -56,12 +57,21 @@ public:
             gen_++;
         }
         cv_.notify_all();
+        std::exception_ptr err;
         t_in_pool = true;
-        work(task, n); // the calling thread takes tasks too
+        try {
+            work(task, n); // the calling thread takes tasks too
+        } catch (...) { // stop handing out tasks, drain the workers, then rethrow with the flag reset
+            err = std::current_exception();
+            next_.store(n);
+        }
         t_in_pool = false;
-        std::unique_lock<std::mutex> g(m_);
-        done_cv_.wait(g, [this] { return left_ == 0; });
-        task_ = nullptr;
+        {
+            std::unique_lock<std::mutex> g(m_);
+            done_cv_.wait(g, [this] { return left_ == 0; });
+            task_ = nullptr;
+        }
+        if (err) std::rethrow_exception(err);
         return true;
     }
 

@@ -1041,34 +1041,30 @@ __device__ __forceinline__ void lane_init(Lane& L)
 // NT: store the item partials non-temporally (the BVH kernels: their 16-B-per-sample partial
 // stream would otherwise push the scene out of the Infinity Cache; C4 52.74-52.86 -> 52.30-52.37
 // ms; the brute-force kernels keep normal stores, die.txt C3 27.5 -> 27.7-27.8 ms with them)
-#ifndef RT_MBCNT
-#define RT_MBCNT 0 // NT (BVH) kernels: a lane's rank among the set lanes of m by v_mbcnt (no lane mask held)
-#endif
-// the set bits of the wave mask m below this lane (v_mbcnt_lo / _hi: no 64-bit lane mask register,
-// which the compiler hoists out of the loop and then spills)
+// The BVH (NT) kernels hold as little per lane as they can: at 7 waves per SIMD every register the
+// refill and shading phases keep live spilled (round 5: 19 VGPRs, 21 GB of scratch writes per C4
+// launch against 2.1 GB of partials).  Four changes, each computing the same values, took that to
+// 2 (profiles/r06/c4_ab.txt, one call: C4 42.99 -> 38.52 ms, WRITE_SIZE 21.2 -> 2.7 GB per launch):
+// * a lane's rank in the item dispenser by v_mbcnt (lanes_below), not a popcount of
+//   m & ((1 << lane) - 1), whose 64-bit lane mask the compiler hoisted out of the loop and spilled;
+// * the pixel's frame x and y in one register (L.fx = x | y << 16; frames < 65536 wide / high);
+// * the pixel's RNG key derived again at each sample start instead of held per lane;
+// * 1/d of every lane's query rebuilt after the shading phase instead of held through it.
+// The brute-force kernels keep their layout (they read the pixel key from the scene's table).
 __device__ __forceinline__ unsigned lanes_below(unsigned long long m)
 {
     return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
-#ifndef RT_PACK_XY
-#define RT_PACK_XY 0 // NT (BVH) kernels: the pixel's frame x and y in one register (L.fx = x | y << 16)
-#endif
 template <bool NT>
 __device__ __forceinline__ int lane_fx(const Lane& L)
 {
-    return (NT && RT_PACK_XY) ? (L.fx & 0xFFFF) : L.fx;
+    return NT ? (L.fx & 0xFFFF) : L.fx;
 }
 template <bool NT>
 __device__ __forceinline__ int lane_fy(const Lane& L)
 {
-    return (NT && RT_PACK_XY) ? (int)((unsigned)L.fx >> 16) : L.fy;
+    return NT ? (int)((unsigned)L.fx >> 16) : L.fy;
 }
-#ifndef RT_ID_AFTER_SHADE
-#define RT_ID_AFTER_SHADE 0
-#endif
-#ifndef RT_PKEY_AT_START
-#define RT_PKEY_AT_START 0 // NT (BVH) kernels: derive the pixel key at each sample start instead of holding it
-#endif
 template <bool NT, class ParT, class SceneT, class CamT>
 __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const SceneT& s, const CamT& cam, int lane,
                                       unsigned total)
@@ -1111,7 +1107,7 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
             fresh = __builtin_amdgcn_readfirstlane(fresh);
         }
         if (need) {
-            const unsigned r = (NT && RT_MBCNT) ? lanes_below(m) : (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+            const unsigned r = NT ? lanes_below(m) : (unsigned)__popcll(m & ((1ull << lane) - 1ull));
             L.item = r < avail ? L.pool_next + r : fresh + (r - avail);
             if (L.item >= total) {
                 L.active = false;
@@ -1145,7 +1141,7 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
                         }
                         L.fy = p.y0 + ((int)bq * p.band_stride + p.band_offset) * p.band + (int)br;
                     }
-                    if (NT && RT_PACK_XY) L.fx |= L.fy << 16; // one register for both (frames < 65536 wide / high)
+                    if (NT) L.fx |= L.fy << 16; // one register for both (frames < 65536 wide / high)
                     // the frame width from the launch record (a scene-specialised build's constant
                     // scene leaves it out, so one build serves every frame size)
                     const unsigned long long px = (unsigned long long)lane_fy<NT>(L) * (unsigned long long)p.scene.width +
@@ -1153,7 +1149,7 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
                     // the brute-force kernels read the key from the scene's table (the same value:
                     // two hash rounds fewer per item open, which runs in most iterations)
                     if (!NT && p.pkeys) L.pkey = p.pkeys[px];
-                    else if (!(NT && RT_PKEY_AT_START)) L.pkey = rt_rng_pixel_key(p.seed_key, px);
+                    else if (!NT) L.pkey = rt_rng_pixel_key(p.seed_key, px);
                 }
             }
         }
@@ -1165,7 +1161,7 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
         }
     }
     if (L.active && L.item_open && !L.live && L.cnt >= 65536u) {
-        if (NT && RT_PKEY_AT_START) // the key from the pixel at every sample start: two registers fewer held
+        if (NT) // the key from the pixel at every sample start: two registers fewer held
             L.pkey = rt_rng_pixel_key(p.seed_key, (unsigned long long)lane_fy<NT>(L) * (unsigned long long)p.scene.width +
                                                       (unsigned long long)lane_fx<NT>(L));
         S.rng = rt_rng_from_pixel_key(L.pkey, p.sample_base + (unsigned long long)L.s_next);
@@ -1493,12 +1489,12 @@ __global__ void __launch_bounds__(256, WIDTH == 4 ? RT_BVH_WAVES : RT_BVH2_WAVES
         if (!busy || __popcll(waiting) >= p.refill) {
             wave_rays += (unsigned)__popcll(__ballot(done)); // one Scene.RayTrace per finished query
             if (done) { // the query finished: the outer records and planes (outside the BVH), then one bounce
-#if !RT_OUTER_AT_START
-                // (a NaN direction, from a vertex-normal triangle, meets nothing: see path_body)
+                // (a NaN direction, from a vertex-normal triangle, meets nothing: see path_body).  Here,
+                // not at the query's start: there it held the query's best hit through the traversal
+                // and measured 48.35 against 38.52 ms (profiles/r06/c4_ab.txt, lowreg_ostart)
                 if (s.n_groups > 0 && !(VN && __builtin_isnan(S.d.x + S.d.y + S.d.z)))
                     test_outer<STATS>((const RT_AS_CONST GroupRec*)pq->groups, (const RT_AS_CONST RectRec*)pq->rects,
                                       (const RT_AS_CONST BoxRec*)pq->frames, S.o, S.d, S.prev, b, cnt.outer);
-#endif
                 for (int i = s.n_bvh; i < s.n_bvh + s.n_pln; i++) {
                     const TestRec tr = tests[i];
                     hit_plane<true>(tr, i, S.o, S.d, S.prev, b);
@@ -1518,7 +1514,6 @@ __global__ void __launch_bounds__(256, WIDTH == 4 ? RT_BVH_WAVES : RT_BVH2_WAVES
             }
             refill<true>(L, S, p, s, *cp, lane, total);
             if (L.live && !trav) { // start the next query
-                if (!RT_ID_AFTER_SHADE) id = v3(slab_rcp(S.d.x), slab_rcp(S.d.y), slab_rcp(S.d.z));
                 ref = s.root;
                 sp = 0;
                 pend = -1;
@@ -1528,16 +1523,11 @@ __global__ void __launch_bounds__(256, WIDTH == 4 ? RT_BVH_WAVES : RT_BVH2_WAVES
                     more = false;
                 }
                 b = query_start<VN>(s, S.prev);
-#if RT_OUTER_AT_START
-                if (s.n_groups > 0 && !(VN && __builtin_isnan(S.d.x + S.d.y + S.d.z)))
-                    test_outer<STATS>((const RT_AS_CONST GroupRec*)pq->groups, (const RT_AS_CONST RectRec*)pq->rects,
-                                      (const RT_AS_CONST BoxRec*)pq->frames, S.o, S.d, S.prev, b, cnt.outer);
-#endif
                 trav = true;
             }
-            // RT_ID_AFTER_SHADE: 1/d of every lane's query rebuilt after the shading phase, so that the
-            // three registers are free inside it (the traversing lanes recompute the same values)
-            if (RT_ID_AFTER_SHADE) id = v3(slab_rcp(S.d.x), slab_rcp(S.d.y), slab_rcp(S.d.z));
+            // 1/d of every lane's query rebuilt after the shading phase, so that the three registers
+            // are free inside it (the traversing lanes recompute the same values)
+            id = v3(slab_rcp(S.d.x), slab_rcp(S.d.y), slab_rcp(S.d.z));
         }
 #if RT_BVH_SPEC
         // Speculative traversal (Aila & Laine 2009): a lane that reaches a leaf keeps it pending and

@@ -704,6 +704,10 @@ BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<
             G.frame_first = (int)o.frames.size();
             G.n_frames = (int16_t)frames.size();
             G.n_boxes = (int16_t)wboxes.size();
+            // the counts are int16 in the record: more would wrap and drop geometry silently
+            if (frames.size() > INT16_MAX || wboxes.size() > INT16_MAX ||
+                frames.size() + wboxes.size() > INT16_MAX)
+                o.overflow = true;
             std::vector<BoxRec> frame_boxes;
             const int frame_box_first = G.frame_first + (int)frames.size() + (int)wboxes.size();
             for (const auto& F : frames) {
@@ -1141,54 +1145,26 @@ int upload_scene(rt_scene* s)
     };
     set_mats(flat.prims);
     set_mats(grouped.prims);
+    // The BVH order: the tree's slots (host: s->sah.order; GPU: gathered on the device), then the
+    // outer records' slots (their records renumbered past the tree), then the planes -- the tail,
+    // built here for both builders.
     std::vector<PrimF> bv;
     std::vector<TestRec> tbv;
-    size_t n_bvh_records = 0;
-    if (s->bvh.builder == RT_BVH_BUILDER_GPU) {
-        // records in ID order, gathered on the device into the GPU builder's leaf order
-        std::vector<PrimF> pid(n);
-        std::vector<TestRec> tid(n);
-        parallel_for(n, [&](int i) {
-            pid[i] = primf(i);
-            tid[i] = testrec(i);
-        });
-        std::vector<int32_t> planes;
-        for (int i = 0; i < n; i++)
-            if (H[i].kind == RT_PRIM_PLANE) planes.push_back(i); // planes follow the BVH's primitives
-        const int nb = s->order_d.n > 0 ? (int)s->order_d.n - (int)planes.size() - 1 : 0;
-        n_bvh_records = (size_t)nb + planes.size();
-        if (!planes.empty())
-            HIP_TRY(hipMemcpy(s->order_d.p + nb, planes.data(), planes.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-        DevBuf<PrimF> pid_d;
-        DevBuf<TestRec> tid_d;
-        set_mats(pid);
-        HIP_TRY(pid_d.upload(pid));
-        HIP_TRY(tid_d.upload(tid));
-        HIP_TRY(s->prims_bvh.reserve(n_bvh_records));
-        HIP_TRY(s->tests_bvh.reserve(n_bvh_records + kTestSpares));
-        HIP_TRY(gather_bvh_records(s->order_d.p, (int)n_bvh_records, pid_d.p, tid_d.p, s->prims_bvh.p, s->tests_bvh.p,
-                                   s->stream));
-        // spare records: the BVH leaf step loads up to kTestSpares past a leaf
-        HIP_TRY(hipMemsetAsync(s->tests_bvh.p + n_bvh_records, 0, kTestSpares * sizeof(TestRec), s->stream));
-        HIP_TRY(hipStreamSynchronize(s->stream));
-        s->order_d.release();
-    } else {
-        for (int i : s->sah.order) {
-            bv.push_back(primf(i));
-            tbv.push_back(testrec(i));
-        }
-        // the outer records' slots follow the tree's (their records renumbered past it)
+    const int n_tree = s->bvh.builder == RT_BVH_BUILDER_GPU
+                           ? (s->order_d.n > 0 ? (int)s->order_d.n - np - 1 : 0)
+                           : (int)s->sah.order.size();
+    {
         BruteOrder& ob = orders.outer;
         if (!ob.groups.empty()) {
-            const int base = (int)bv.size(), n_slots = (int)ob.prims.size() - np;
+            const int n_slots = (int)ob.prims.size() - np;
             bv.insert(bv.end(), ob.prims.begin(), ob.prims.begin() + n_slots);
             tbv.insert(tbv.end(), ob.tests.begin(), ob.tests.begin() + n_slots);
-            for (RectRec& r : ob.rects) r.sg += base << 1;
+            for (RectRec& r : ob.rects) r.sg += n_tree << 1;
             const GroupRec& G = ob.groups[0];
             for (int j = G.frame_first + G.n_frames; j < G.frame_first + G.n_frames + G.n_boxes; j++) {
                 BoxRec B;
                 std::memcpy(&B, &ob.frames[j], sizeof B);
-                B.sg0 += base << 1;
+                B.sg0 += n_tree << 1;
                 std::memcpy(&ob.frames[j], &B, sizeof B);
             }
         }
@@ -1197,9 +1173,46 @@ int upload_scene(rt_scene* s)
                 bv.push_back(primf(i));
                 tbv.push_back(testrec(i));
             }
-        n_bvh_records = bv.size();
     }
+    const size_t n_bvh_records = (size_t)n_tree + bv.size();
     set_mats(bv);
+    if (s->bvh.builder == RT_BVH_BUILDER_GPU) {
+        // the tree's records in ID order, gathered on the device into the GPU builder's leaf order
+        std::vector<PrimF> pid(n);
+        std::vector<TestRec> tid(n);
+        parallel_for(n, [&](int i) {
+            pid[i] = primf(i);
+            tid[i] = testrec(i);
+        });
+        DevBuf<PrimF> pid_d;
+        DevBuf<TestRec> tid_d;
+        set_mats(pid);
+        HIP_TRY(pid_d.upload(pid));
+        HIP_TRY(tid_d.upload(tid));
+        HIP_TRY(s->prims_bvh.reserve(n_bvh_records));
+        HIP_TRY(s->tests_bvh.reserve(n_bvh_records + kTestSpares));
+        HIP_TRY(gather_bvh_records(s->order_d.p, n_tree, pid_d.p, tid_d.p, s->prims_bvh.p, s->tests_bvh.p, s->stream));
+        if (!bv.empty()) {
+            HIP_TRY(hipMemcpyAsync(s->prims_bvh.p + n_tree, bv.data(), bv.size() * sizeof(PrimF), hipMemcpyHostToDevice,
+                                   s->stream));
+            HIP_TRY(hipMemcpyAsync(s->tests_bvh.p + n_tree, tbv.data(), tbv.size() * sizeof(TestRec),
+                                   hipMemcpyHostToDevice, s->stream));
+        }
+        // spare records: the BVH leaf step loads up to kTestSpares past a leaf
+        HIP_TRY(hipMemsetAsync(s->tests_bvh.p + n_bvh_records, 0, kTestSpares * sizeof(TestRec), s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        s->order_d.release();
+    } else {
+        std::vector<PrimF> tree(n_tree);
+        std::vector<TestRec> ttree(n_tree);
+        parallel_for(n_tree, [&](int k) {
+            tree[k] = primf(s->sah.order[k]);
+            ttree[k] = testrec(s->sah.order[k]);
+        });
+        set_mats(tree);
+        bv.insert(bv.begin(), tree.begin(), tree.end());
+        tbv.insert(tbv.begin(), ttree.begin(), ttree.end());
+    }
     HIP_TRY(s->prims_d.upload(pd));
     HIP_TRY(s->xf_d.upload(xd));
     HIP_TRY(s->prims_bf.upload(flat.prims));
@@ -1222,11 +1235,11 @@ int upload_scene(rt_scene* s)
         HIP_TRY(s->tests_bvh.upload(tbv));
         HIP_TRY(s->nodes.upload(s->sah.nodes));
         HIP_TRY(s->nodes4.upload(s->bvh4.nodes));
-        if (!orders.outer.groups.empty()) {
-            HIP_TRY(s->rects_bvh.upload(orders.outer.rects));
-            HIP_TRY(s->frames_bvh.upload(orders.outer.frames));
-            HIP_TRY(s->groups_bvh.upload(orders.outer.groups));
-        }
+    }
+    if (!orders.outer.groups.empty()) {
+        HIP_TRY(s->rects_bvh.upload(orders.outer.rects));
+        HIP_TRY(s->frames_bvh.upload(orders.outer.frames));
+        HIP_TRY(s->groups_bvh.upload(orders.outer.groups));
     }
     HIP_TRY(s->xf.upload(xf));
     HIP_TRY(s->mats.upload(mats));
@@ -1843,6 +1856,52 @@ std::atomic<int> g_builder{RT_BVH_BUILDER_AUTO};
 // and 8 % of the render rate, against 0.4 s of build time saved.
 constexpr int kGpuBuildMin = 1 << 22;
 
+// Which axis-aligned rectangles become outer records.  Only large ones pay: a wall whose box
+// overlaps the whole scene sits near the root of any tree, while a small cube face is cheap inside
+// it and would cost every query a test outside it (test_outer is linear in the group).  So a
+// rectangle qualifies when its area is at least 1/kOuterAreaDiv of the scene box's largest face,
+// and at most kOuterMax of them (largest first) are taken.  C4: the room's six walls and the
+// light box's five faces (the smallest, 0.75 x 0.1, is 1/213 of the 4 x 4 face).  None, or all
+// of the BVH primitives, leaves the tree as it is.
+constexpr int kOuterMax = 64;
+constexpr double kOuterAreaDiv = 1024.0;
+
+void select_outer(const std::vector<HostPrim>& H, std::vector<char>& out)
+{
+    out.clear();
+    const int n = (int)H.size();
+    float slo[3] = {INFINITY, INFINITY, INFINITY}, shi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    int nb = 0;
+    std::vector<std::pair<double, int>> cand;
+    for (int i = 0; i < n; i++) {
+        if (H[i].kind == RT_PRIM_PLANE) continue;
+        nb++;
+        float lo[3], hi[3];
+        sah_prim_box(H[i], lo, hi);
+        for (int k = 0; k < 3; k++) {
+            slo[k] = std::min(slo[k], lo[k]);
+            shi[k] = std::max(shi[k], hi[k]);
+        }
+        const int k = rect_axis_of(H[i]);
+        if (k < 0) continue;
+        const double a = (double)(hi[(k + 1) % 3] - lo[(k + 1) % 3]) * (double)(hi[(k + 2) % 3] - lo[(k + 2) % 3]);
+        cand.push_back({a, i});
+    }
+    double face = 0.0;
+    for (int k = 0; k < 3; k++)
+        face = std::max(face, (double)(shi[(k + 1) % 3] - slo[(k + 1) % 3]) * (double)(shi[(k + 2) % 3] - slo[(k + 2) % 3]));
+    // largest first, then by ID (a stable choice at the cap)
+    std::sort(cand.begin(), cand.end(), [](const auto& a, const auto& b) { return a.first != b.first ? a.first > b.first : a.second < b.second; });
+    std::vector<char> m(n, 0);
+    int k = 0;
+    for (const auto& c : cand) {
+        if (k == kOuterMax || !(c.first * kOuterAreaDiv >= face)) break;
+        m[c.second] = 1;
+        k++;
+    }
+    if (k > 0 && k < nb) out = std::move(m);
+}
+
 int builder_for(int n_bvh)
 {
     int b = g_builder.load();
@@ -1874,15 +1933,10 @@ int build_bvhs(rt_scene* s)
     // large boxes overlap the whole scene near the root (tools/bvh_sim.cpp on C4's mesh: node
     // visits per query 8.75 -> 7.88, primitive tests 5.33 -> 2.46; measured: C4 46.5 -> 44.0 ms,
     // nodes 9.16 -> 8.34 and leaf tests 5.75 -> 2.88 per ray segment).  RTCORE_BVH_OUTER=0: off.
-    bool outer_on = nb > 4096 && s->bvh.builder == RT_BVH_BUILDER_HOST;
+    bool outer_on = nb > 4096;
     if (const char* e = getenv("RTCORE_BVH_OUTER")) outer_on = outer_on && atoi(e) != 0;
     s->bvh_outer.clear();
-    if (outer_on) {
-        std::vector<char> m(n, 0);
-        int k = 0;
-        for (int i = 0; i < n; i++) k += (m[i] = rect_axis_of(H[i]) >= 0);
-        if (k > 0 && k < nb) s->bvh_outer = std::move(m);
-    }
+    if (outer_on) select_outer(H, s->bvh_outer);
     // leaves of <= 3 primitives, <= 2 with outer records (C4, round 2: leaves of <= 2, 3, 4, 6, 8 ->
     // 70.6, 70.5, 72.2, 76.1, 80.2 ms; round 5 with outer records: 2 / 3 / 4 -> 43.8 / 44.0 / 47.2)
     int max_leaf = n > 256 && s->bvh_outer.empty() ? 3 : 2;
@@ -1908,19 +1962,22 @@ int build_bvhs(rt_scene* s)
         s->bvh.stack4 = s->bvh4.stack_need;
         return RT_OK;
     }
-    std::vector<float4> lo(nb), hi(nb);
-    parallel_for(nb, [&](int k) {
+    const int n_planes = n - nb;
+    if (!s->bvh_outer.empty()) // the outer records stay out of the GPU builder's tree too
+        ids.erase(std::remove_if(ids.begin(), ids.end(), [&](int32_t i) { return s->bvh_outer[i] != 0; }), ids.end());
+    const int n_tree = (int)ids.size();
+    std::vector<float4> lo(n_tree), hi(n_tree);
+    parallel_for(n_tree, [&](int k) {
         float l[3], h[3];
         sah_prim_box(H[ids[k]], l, h);
         lo[k] = make_float4(l[0], l[1], l[2], 0.0f);
         hi[k] = make_float4(h[0], h[1], h[2], 0.0f);
     });
-    int n_planes = n - nb;
     GpuBvh g;
-    HIP_TRY(build_bvh_gpu(lo.data(), hi.data(), ids.data(), nb, max_leaf, n_planes + 1, s->stream, g));
+    HIP_TRY(build_bvh_gpu(lo.data(), hi.data(), ids.data(), n_tree, max_leaf, n_planes + 1, s->stream, g));
     s->nodes.adopt(g.nodes, g.n_nodes);
     s->nodes4.adopt(g.nodes4, g.n_nodes4);
-    s->order_d.adopt(g.order, (size_t)nb + n_planes + 1);
+    s->order_d.adopt(g.order, (size_t)n_tree + n_planes + 1);
     s->bvh.n_nodes2 = g.n_nodes;
     s->bvh.root2 = g.root;
     s->bvh.depth2 = g.depth;
@@ -2443,6 +2500,10 @@ int rt_scene_create(const rt_scene_params* params, const rt_prim* prims, int32_t
         set_error("rt_scene_create: width and height must be positive");
         return RT_ERR_ARG;
     }
+    if (params->width > 65535 || params->height > 65535) { // the BVH kernels pack a pixel's x, y in 16 bits each
+        set_error("rt_scene_create: width and height must be at most 65535");
+        return RT_ERR_ARG;
+    }
     for (int i = 0; i < n_prims; i++)
         if (prims[i].kind < 0 || prims[i].kind > 2) {
             set_error("rt_scene_create: unknown primitive kind at index " + std::to_string(i));
@@ -2845,25 +2906,45 @@ struct rt_frame {
     std::vector<int> rows;            // rows of device g's band set
     size_t slot_pix = 0, slot_bytes = 0;
     std::vector<rt_scene*> scenes;
-    std::vector<unsigned char*> sendb; // per device: one gather slot, Σr | Σg | Σb fp64, samples, misses u32
-    unsigned char* recvb = nullptr;    // device 0: n slots (n > 1)
-    unsigned char* host = nullptr;     // pinned copy of the gathered slots
-    std::vector<ncclComm_t> comms;
-    std::vector<unsigned long long> rays_h;
+    std::vector<ncclComm_t> comms; // one rank per device (n = 1 too: one code path, a local copy)
+    // Two pipeline stages (rt_frame_submit / rt_frame_collect): stage j holds every device's gather
+    // slot, device 0's receive buffer (n slots), the pinned host copy of the gathered slots and of
+    // the devices' ray counts, and the event that says the host copy has landed.
+    static constexpr int kStages = 2;
+    struct Stage {
+        std::vector<unsigned char*> sendb; // per device: Σr | Σg | Σb fp64, samples, misses u32
+        unsigned char* recvb = nullptr;    // device 0
+        unsigned char* host = nullptr;     // pinned: n slots, then n ray counts
+        hipEvent_t gathered = nullptr;     // device 0's render stream: the gather is complete
+        hipEvent_t landed = nullptr;       // device 0's copy stream: the host copy is complete
+        std::vector<hipEvent_t> rays_ev;   // per device: its ray count has been copied
+    } st[kStages];
+    hipStream_t copy_stream = nullptr;     // device 0: host copies, off the render streams
+    unsigned long long submitted = 0, collected = 0; // renders queued / merged (at most kStages apart)
+    int inject = 0;                        // rt_frame_inject_fault (tests)
 
+    unsigned long long* host_rays(int j) { return reinterpret_cast<unsigned long long*>(st[j].host + slot_bytes * n); }
     ~rt_frame()
     {
         for (ncclComm_t c : comms) (void)ncclCommDestroy(c);
-        for (int g = 0; g < (int)sendb.size(); g++)
-            if (sendb[g]) {
-                (void)hipSetDevice(scenes[g]->device);
-                (void)hipFree(sendb[g]);
-            }
-        if (recvb) {
-            (void)hipSetDevice(scenes[0]->device);
-            (void)hipFree(recvb);
+        for (auto& S : st) {
+            for (int g = 0; g < (int)S.sendb.size(); g++)
+                if (S.sendb[g]) {
+                    (void)hipSetDevice(scenes[g]->device);
+                    (void)hipFree(S.sendb[g]);
+                }
+            for (int g = 0; g < (int)S.rays_ev.size(); g++)
+                if (S.rays_ev[g]) {
+                    (void)hipSetDevice(scenes[g]->device);
+                    (void)hipEventDestroy(S.rays_ev[g]);
+                }
+            if (!scenes.empty() && scenes[0]) (void)hipSetDevice(scenes[0]->device);
+            if (S.recvb) (void)hipFree(S.recvb);
+            if (S.landed) (void)hipEventDestroy(S.landed);
+            if (S.gathered) (void)hipEventDestroy(S.gathered);
+            if (S.host) (void)hipHostFree(S.host);
         }
-        if (host) (void)hipHostFree(host);
+        if (copy_stream) (void)hipStreamDestroy(copy_stream);
         for (rt_scene* s : scenes)
             if (s) rt_scene_destroy(s);
     }
@@ -3052,8 +3133,10 @@ int rt_frame_create(const rt_scene_params* params, const rt_prim* prims, int32_t
     f->slot_pix = (size_t)band_slot_rows(f->H, f->band, n_gpus) * f->W;
     f->slot_bytes = f->slot_pix * (3 * sizeof(double) + 2 * sizeof(uint32_t));
     f->scenes.assign(n_gpus, nullptr);
-    f->sendb.assign(n_gpus, nullptr);
-    f->rays_h.assign(n_gpus, 0);
+    for (auto& S : f->st) {
+        S.sendb.assign(n_gpus, nullptr);
+        S.rays_ev.assign(n_gpus, nullptr);
+    }
     std::vector<int> devs(n_gpus);
     for (int g = 0; g < n_gpus; g++) {
         devs[g] = g;
@@ -3061,18 +3144,25 @@ int rt_frame_create(const rt_scene_params* params, const rt_prim* prims, int32_t
         if (rc == RT_OK) rc = rt_scene_set_camera(f->scenes[g], camera);
         if (rc != RT_OK) return rc;
         HIP_TRY(hipSetDevice(g));
-        HIP_TRY(hipMalloc(&f->sendb[g], f->slot_bytes));
-    }
-    HIP_TRY(hipHostMalloc(&f->host, f->slot_bytes * n_gpus, hipHostMallocDefault));
-    if (n_gpus > 1) {
-        HIP_TRY(hipSetDevice(0));
-        HIP_TRY(hipMalloc(&f->recvb, f->slot_bytes * n_gpus));
-        f->comms.assign(n_gpus, nullptr);
-        if (ncclCommInitAll(f->comms.data(), n_gpus, devs.data()) != ncclSuccess) {
-            f->comms.clear();
-            set_error("rt_frame_create: ncclCommInitAll failed");
-            return RT_ERR_NCCL;
+        for (auto& S : f->st) {
+            HIP_TRY(hipMalloc(&S.sendb[g], f->slot_bytes));
+            HIP_TRY(hipEventCreateWithFlags(&S.rays_ev[g], hipEventDisableTiming));
         }
+    }
+    HIP_TRY(hipSetDevice(0));
+    HIP_TRY(hipStreamCreateWithFlags(&f->copy_stream, hipStreamNonBlocking));
+    for (auto& S : f->st) {
+        HIP_TRY(hipMalloc(&S.recvb, f->slot_bytes * n_gpus));
+        HIP_TRY(hipHostMalloc(&S.host, f->slot_bytes * n_gpus + sizeof(unsigned long long) * n_gpus,
+                              hipHostMallocDefault));
+        HIP_TRY(hipEventCreateWithFlags(&S.landed, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&S.gathered, hipEventDisableTiming));
+    }
+    f->comms.assign(n_gpus, nullptr);
+    if (ncclCommInitAll(f->comms.data(), n_gpus, devs.data()) != ncclSuccess) {
+        f->comms.clear();
+        set_error("rt_frame_create: ncclCommInitAll failed");
+        return RT_ERR_NCCL;
     }
     *out = f.release();
     return RT_OK;
@@ -3091,6 +3181,144 @@ int rt_frame_set_camera(rt_frame* f, const rt_camera* camera)
     return RT_OK;
 }
 
+namespace {
+
+// Drops every queued stage after a failure: waits for the devices' streams, so that no queued
+// copy still writes a stage's buffers, and restarts the pipeline empty.
+void frame_drain(rt_frame* f)
+{
+    for (rt_scene* s : f->scenes) {
+        (void)hipSetDevice(s->device);
+        (void)hipStreamSynchronize(s->stream);
+    }
+    (void)hipSetDevice(f->scenes[0]->device);
+    (void)hipStreamSynchronize(f->copy_stream);
+    f->submitted = f->collected = 0;
+}
+
+// The gather of stage j: every device's slot onto device 0, one grouped RCCL call.  The group is
+// closed on every path (an open group would swallow the next call's gathers).
+int frame_gather(rt_frame* f, int j)
+{
+    if (ncclGroupStart() != ncclSuccess) {
+        set_error("rt_frame_render: ncclGroupStart failed");
+        return RT_ERR_NCCL;
+    }
+    int rc = RT_OK;
+    for (int g = 0; g < f->n && rc == RT_OK; g++) {
+        if (f->inject == 1) { // rt_frame_inject_fault: a failure inside the group, before any gather
+            f->inject = 0;
+            set_error("rt_frame_render: injected fault inside the gather group");
+            rc = RT_ERR_HIP;
+            break;
+        }
+        const hipError_t e = hipSetDevice(f->scenes[g]->device);
+        if (e != hipSuccess) {
+            set_error(std::string("rt_frame_render: ") + hipGetErrorString(e));
+            rc = RT_ERR_HIP;
+            break;
+        }
+        if (ncclGather(f->st[j].sendb[g], g == 0 ? f->st[j].recvb : nullptr, f->slot_bytes, ncclUint8, 0, f->comms[g],
+                       f->scenes[g]->stream) != ncclSuccess) {
+            set_error("rt_frame_render: ncclGather failed");
+            rc = RT_ERR_NCCL;
+        }
+    }
+    if (ncclGroupEnd() != ncclSuccess && rc == RT_OK) {
+        set_error("rt_frame_render: ncclGather failed");
+        rc = RT_ERR_NCCL;
+    }
+    return rc;
+}
+
+int frame_submit(rt_frame* f, int32_t spp, uint64_t seed, uint64_t sample_base)
+{
+    const int j = (int)(f->submitted % rt_frame::kStages);
+    auto& S = f->st[j];
+    rt_scene* s0 = f->scenes[0];
+    // every device renders its band set into its slot of stage j, concurrently (asynchronous launches);
+    // the stage's previous host copy has been collected (at most kStages in flight), so its buffers
+    // are free once device 0's copy stream has passed it, which the render streams wait for
+    for (int g = 0; g < f->n; g++) {
+        rt_scene* s = f->scenes[g];
+        HIP_TRY(hipSetDevice(s->device));
+        if (g == 0) HIP_TRY(hipStreamWaitEvent(s->stream, S.landed, 0));
+        HIP_TRY(hipMemsetAsync(S.sendb[g], 0, f->slot_bytes, s->stream));
+        HIP_TRY(hipMemsetAsync(s->rays.p, 0, sizeof(unsigned long long), s->stream));
+        if (f->rows[g] > 0) {
+            int rc = render_band_set(s, f->band, f->n, g, f->rows[g], f->slot_pix, spp, seed, sample_base, S.sendb[g],
+                                     s->rays.p, s->stream);
+            if (rc != RT_OK) return rc;
+        }
+        // the ray count, before the next stage's render zeroes it (pinned: the copy is asynchronous)
+        HIP_TRY(hipMemcpyAsync(f->host_rays(j) + g, s->rays.p, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                               s->stream));
+        HIP_TRY(hipEventRecord(S.rays_ev[g], s->stream));
+    }
+    // the slots meet on device 0 through one RCCL gather over xGMI
+    int rc = frame_gather(f, j);
+    if (rc != RT_OK) return rc;
+    // the host copy on device 0's copy stream, so that the next stage's render does not queue behind it
+    HIP_TRY(hipSetDevice(s0->device));
+    HIP_TRY(hipEventRecord(S.gathered, s0->stream));
+    HIP_TRY(hipStreamWaitEvent(f->copy_stream, S.gathered, 0));
+    HIP_TRY(hipMemcpyAsync(S.host, S.recvb, f->slot_bytes * f->n, hipMemcpyDeviceToHost, f->copy_stream));
+    HIP_TRY(hipEventRecord(S.landed, f->copy_stream));
+    f->submitted++;
+    return RT_OK;
+}
+
+int frame_collect(rt_frame* f, rt_color* sum_rgb, uint32_t* samples, uint32_t* misses, uint64_t* rays_out)
+{
+    const int j = (int)(f->collected % rt_frame::kStages);
+    auto& S = f->st[j];
+    HIP_TRY(hipSetDevice(f->scenes[0]->device));
+    HIP_TRY(hipEventSynchronize(S.landed));
+    for (int g = 0; g < f->n; g++) {
+        HIP_TRY(hipSetDevice(f->scenes[g]->device));
+        HIP_TRY(hipEventSynchronize(S.rays_ev[g]));
+    }
+    for (int g = 0; g < f->n; g++)
+        scatter_band_set(S.host + f->slot_bytes * g, f->slot_pix, f->W, f->H, f->band, f->n, g, sum_rgb, samples,
+                         misses);
+    if (rays_out)
+        for (int g = 0; g < f->n; g++) *rays_out += f->host_rays(j)[g];
+    f->collected++;
+    return RT_OK;
+}
+
+} // namespace
+
+int rt_frame_submit(rt_frame* f, int32_t spp, uint64_t seed, uint64_t sample_base)
+{
+    if (!f || spp <= 0) {
+        set_error("rt_frame_submit: bad argument");
+        return RT_ERR_ARG;
+    }
+    if (f->submitted - f->collected >= (unsigned long long)rt_frame::kStages) {
+        set_error("rt_frame_submit: two renders in flight; rt_frame_collect the oldest first");
+        return RT_ERR_STATE;
+    }
+    const int rc = frame_submit(f, spp, seed, sample_base);
+    if (rc != RT_OK) frame_drain(f);
+    return rc;
+}
+
+int rt_frame_collect(rt_frame* f, rt_color* sum_rgb, uint32_t* samples, uint32_t* misses, uint64_t* rays_out)
+{
+    if (!f || !sum_rgb || !samples || !misses) {
+        set_error("rt_frame_collect: bad argument");
+        return RT_ERR_ARG;
+    }
+    if (f->collected == f->submitted) {
+        set_error("rt_frame_collect: nothing submitted");
+        return RT_ERR_STATE;
+    }
+    const int rc = frame_collect(f, sum_rgb, samples, misses, rays_out);
+    if (rc != RT_OK) frame_drain(f);
+    return rc;
+}
+
 int rt_frame_render(rt_frame* f, int32_t spp, uint64_t seed, uint64_t sample_base, rt_color* sum_rgb,
                     uint32_t* samples, uint32_t* misses, uint64_t* rays_out)
 {
@@ -3099,54 +3327,22 @@ int rt_frame_render(rt_frame* f, int32_t spp, uint64_t seed, uint64_t sample_bas
         return RT_ERR_ARG;
     }
     if (spp == 0) return RT_OK;
-    // every device renders its band set into its slot, concurrently (launches are asynchronous)
-    for (int g = 0; g < f->n; g++) {
-        rt_scene* s = f->scenes[g];
-        HIP_TRY(hipSetDevice(s->device));
-        HIP_TRY(hipMemsetAsync(f->sendb[g], 0, f->slot_bytes, s->stream));
-        HIP_TRY(hipMemsetAsync(s->rays.p, 0, sizeof(unsigned long long), s->stream));
-        if (f->rows[g] == 0) continue;
-        int rc = render_band_set(s, f->band, f->n, g, f->rows[g], f->slot_pix, spp, seed, sample_base, f->sendb[g],
-                                 s->rays.p, s->stream);
-        if (rc != RT_OK) return rc;
+    if (f->submitted != f->collected) {
+        set_error("rt_frame_render: renders submitted and not collected");
+        return RT_ERR_STATE;
     }
-    // the slots meet on device 0 through one RCCL gather over xGMI
-    const unsigned char* src = f->sendb[0];
-    if (f->n > 1) {
-        if (ncclGroupStart() != ncclSuccess) {
-            set_error("rt_frame_render: ncclGroupStart failed");
-            return RT_ERR_NCCL;
-        }
-        bool ok = true;
-        for (int g = 0; g < f->n; g++) {
-            HIP_TRY(hipSetDevice(f->scenes[g]->device));
-            ok &= ncclGather(f->sendb[g], g == 0 ? f->recvb : nullptr, f->slot_bytes, ncclUint8, 0, f->comms[g],
-                             f->scenes[g]->stream) == ncclSuccess;
-        }
-        ok &= ncclGroupEnd() == ncclSuccess;
-        if (!ok) {
-            set_error("rt_frame_render: ncclGather failed");
-            return RT_ERR_NCCL;
-        }
-        src = f->recvb;
+    int rc = rt_frame_submit(f, spp, seed, sample_base);
+    if (rc == RT_OK) rc = rt_frame_collect(f, sum_rgb, samples, misses, rays_out);
+    return rc;
+}
+
+int rt_frame_inject_fault(rt_frame* f, int32_t point)
+{
+    if (!f || point < 0 || point > 1) {
+        set_error("rt_frame_inject_fault: bad argument");
+        return RT_ERR_ARG;
     }
-    for (int g = 0; g < f->n; g++) {
-        rt_scene* s = f->scenes[g];
-        HIP_TRY(hipSetDevice(s->device));
-        HIP_TRY(hipMemcpyAsync(&f->rays_h[g], s->rays.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s->stream));
-    }
-    rt_scene* s0 = f->scenes[0];
-    HIP_TRY(hipSetDevice(s0->device));
-    HIP_TRY(hipMemcpyAsync(f->host, src, f->slot_bytes * f->n, hipMemcpyDeviceToHost, s0->stream));
-    for (int g = 0; g < f->n; g++) {
-        HIP_TRY(hipSetDevice(f->scenes[g]->device));
-        HIP_TRY(hipStreamSynchronize(f->scenes[g]->stream));
-    }
-    for (int g = 0; g < f->n; g++)
-        scatter_band_set(f->host + f->slot_bytes * g, f->slot_pix, f->W, f->H, f->band, f->n, g, sum_rgb, samples,
-                         misses);
-    if (rays_out)
-        for (auto r : f->rays_h) *rays_out += r;
+    f->inject = point;
     return RT_OK;
 }
 
@@ -3158,6 +3354,10 @@ void rt_frame_destroy(rt_frame* f)
             (void)hipSetDevice(s->device);
             (void)hipStreamSynchronize(s->stream);
         }
+    if (f->copy_stream) {
+        (void)hipSetDevice(f->scenes[0]->device);
+        (void)hipStreamSynchronize(f->copy_stream);
+    }
     delete f;
 }
 

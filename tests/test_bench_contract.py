@@ -6,6 +6,7 @@ import os
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -67,3 +68,36 @@ def test_bench_frame_split_single_process():
     d = _last_json(r.stdout)
     assert d["n_gpus"] == 1 and d["value"] > 0 and d["steps"] == 2 and d["scaling"] == "weak"
     assert "rt_frame" in d["config"]["parallelism"] and d["config"]["workload"].startswith("bounce.txt")
+
+
+def test_bench_gpus2_without_launcher_starts_its_ranks(tmp_path):
+    """`bench.py --gpus 2` with no WORLD_SIZE starts its own two ranks (fresh processes) instead of
+    quietly measuring one GPU: the line says n_gpus 2, and the gathered frame of the two ranks'
+    band sets (gloo, both on device 0) equals, bit for bit, one rank rendering the same frame."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["RTCORE_BENCH_SAME_DEVICE"] = "1"
+    common = ["--config", "bounce256", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    two, one = tmp_path / "two.npz", tmp_path / "one.npz"
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--spp", "4", "--dump", str(two)] + common,
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 2 and d["multi_gpu"]["world_size"] == 2
+    # one rank, the same frame: 2 x 4 samples per pixel per step, the same sample indices
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--spp", "8", "--dump", str(one)] + common,
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert _last_json(r.stdout)["n_gpus"] == 1
+    a, b = np.load(two), np.load(one)
+    assert int(a["samples"].sum() + a["misses"].sum()) == 256 * 256 * 8 * 3
+    for k in ("sum", "samples", "misses"):
+        assert np.array_equal(a[k], b[k]), k
+
+
+def test_bench_world_size_must_match_gpus():
+    """A launcher world that disagrees with --gpus is refused (rc != 0), never reported as n_gpus 1."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0", "--spp", "4",
+                        "--config", "bounce256", "--no-cpu-baseline"], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode != 0 and '"n_gpus"' not in r.stdout

@@ -81,6 +81,9 @@ def test_mesh1m_window_against_oracle(rc, mesh1m, mode, builder):
     gpu = rc.GpuRaytracer(scene, 0, size=MESH_SIZE, traversal=getattr(rc, "RT_TRAVERSAL_" + mode),
                           builder=getattr(rc, "RT_BVH_BUILDER_" + builder))
     assert gpu.info().traversal == getattr(rc, "RT_TRAVERSAL_" + mode)
+    # the room's six walls and the light box's five faces stay out of either builder's tree
+    assert gpu.build_stats()["outer_prims"] == 11
+    gpu.check_bvh()
     for w in MESH_WINDOWS:
         out = gpu.render_tile(*w, 16, seed=21)
         assert (out[2] == 0).all()  # every camera sample meets the room or the field

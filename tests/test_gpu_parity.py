@@ -281,24 +281,58 @@ def test_traversal_modes_agree(rc, scenes, name, mode):
     assert np.allclose(sa, sb, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("mode,nx", [("BVH", 41), ("BVH2", 41), ("GROUPED", 41), ("BVH", 71), ("BVH2", 71)])
-def test_traversal_modes_agree_mesh(rc, mode, nx):
+@pytest.mark.parametrize("mode,nx,builder", [("BVH", 41, "HOST"), ("BVH2", 41, "HOST"), ("GROUPED", 41, "HOST"),
+                                             ("BVH", 71, "HOST"), ("BVH2", 71, "HOST"), ("BVH", 71, "GPU"),
+                                             ("BVH2", 71, "GPU")])
+def test_traversal_modes_agree_mesh(rc, mode, nx, builder):
     """The same on a small procedural height field (3,200 triangles; 5,600 at nx = 71, where the
-    BVH kernels test the room and the light box as outer records): BVH == brute force up to ties
-    on shared triangle edges."""
+    BVH kernels test the room and the light box as outer records, with either builder's tree):
+    BVH == brute force up to ties on shared triangle edges."""
     from raytracercore_amd.scenes import mesh_scene_text
 
     scene = rc.SceneLoader.from_text(mesh_scene_text(nx=nx, ny=41))
     a = rc.GpuRaytracer(scene, 0, size=(96, 64), traversal=rc.RT_TRAVERSAL_BRUTE)
-    b = rc.GpuRaytracer(scene, 0, size=(96, 64), traversal=getattr(rc, "RT_TRAVERSAL_" + mode))
+    b = rc.GpuRaytracer(scene, 0, size=(96, 64), traversal=getattr(rc, "RT_TRAVERSAL_" + mode),
+                        builder=getattr(rc, "RT_BVH_BUILDER_" + builder))
     assert b.info().traversal == getattr(rc, "RT_TRAVERSAL_" + mode)
+    assert b.info().bvh_builder == getattr(rc, "RT_BVH_BUILDER_" + builder)
     assert (b.build_stats()["outer_prims"] == 11) == (nx == 71)
+    b.check_bvh()
     sa, na, ma, ra = a.render_tile(0, 0, 96, 64, 16, seed=4)
     sb, nb, mb, rb = b.render_tile(0, 0, 96, 64, 16, seed=4)
     assert abs(int(ma.sum()) - int(mb.sum())) <= 2
     assert abs(ra - rb) <= 2e-3 * ra
     same = np.isclose(sa, sb, rtol=1e-4, atol=1e-4).all(axis=-1).mean()
     assert same > 0.99, same
+
+
+def test_outer_records_leave_small_cubes_in_the_tree(rc):
+    """Outer records are only the large axis-aligned rectangles: 300 small cubes
+    (1,800 axis-aligned faces) beside a 3,200-triangle height field in the bounce room stay in the
+    tree, while the room's walls and the light box's faces (11) leave it; the render still equals
+    brute force up to ties."""
+    from raytracercore_amd.scenes import mesh_scene_text
+
+    rng = np.random.default_rng(5)
+    cubes = ["\ndiffuse .3 .5 .7\nspecular .1 .1 .1\n"]
+    for x, y, z in rng.uniform([-1.8, -1.8, -1.6], [1.8, 1.8, -0.5], size=(300, 3)):
+        cubes.append(f"cube {x:.4f} {y:.4f} {z:.4f} .06 .06 .06 all\n")
+    scene = rc.SceneLoader.from_text(mesh_scene_text(nx=41, ny=41) + "".join(cubes))
+    assert scene.n_prims == 5 + 6 + 3200 + 1800  # light box, room, field, cubes
+    a = rc.GpuRaytracer(scene, 0, size=(96, 64), traversal=rc.RT_TRAVERSAL_BRUTE)
+    for builder in ("HOST", "GPU"):
+        b = rc.GpuRaytracer(scene, 0, size=(96, 64), traversal=rc.RT_TRAVERSAL_BVH,
+                            builder=getattr(rc, "RT_BVH_BUILDER_" + builder))
+        st = b.build_stats()
+        assert st["outer_prims"] == 11, st["outer_prims"]
+        b.check_bvh()
+        sa, na, ma, ra = a.render_tile(0, 0, 96, 64, 16, seed=4)
+        sb, nb, mb, rb = b.render_tile(0, 0, 96, 64, 16, seed=4)
+        assert abs(int(ma.sum()) - int(mb.sum())) <= 2
+        assert abs(ra - rb) <= 2e-3 * ra
+        same = np.isclose(sa, sb, rtol=1e-4, atol=1e-4).all(axis=-1).mean()
+        assert same > 0.99, same
+        b.close()
 
 
 def _builder_scene(rc, scenes, name):
@@ -487,6 +521,54 @@ def test_frame_progressive_sample_base(rc, scenes):
     s2, n2, m2, r2 = gpu.render_tile(0, 0, 72, 56, 16, seed=2)
     assert np.array_equal(n, n2) and np.array_equal(m, m2) and out[3] + r == r2
     assert np.allclose(s, s2, rtol=1e-5, atol=1e-5)
+
+
+def test_frame_submit_collect_pipeline(rc, scenes):
+    """rt_frame_submit / rt_frame_collect with render k+1 submitted before render k is collected
+    (the two-stage pipeline) accumulate bit for bit what sequential rt_frame_render calls do; a
+    third submit with two in flight is refused (RT_ERR_STATE) and the pipeline still works."""
+    scene = scenes["bounce.txt"]
+    W, H = 80, 48
+    f = rc.GpuFrame(scene, 0, n_gpus=1, size=(W, H))
+    zero = lambda: (np.zeros((W, H, 3)), np.zeros((W, H), np.uint32), np.zeros((W, H), np.uint32))
+    seq = zero()
+    rays_seq = sum(f.render(4, seed=3, sample_base=4 * k, out=seq)[3] for k in range(5))
+    pip = zero()
+    rays_pip = 0
+    f.submit(4, seed=3, sample_base=0)
+    for k in range(5):
+        if k + 1 < 5:
+            f.submit(4, seed=3, sample_base=4 * (k + 1))
+        if k == 2:
+            with pytest.raises(rc.RtError, match="in flight"):
+                f.submit(4, seed=3, sample_base=999)
+        rays_pip += f.collect(pip)[3]
+    with pytest.raises(rc.RtError, match="nothing submitted"):
+        f.collect(pip)
+    f.close()
+    assert rays_pip == rays_seq
+    for a, b in zip(pip, seq):
+        assert np.array_equal(a, b)
+    assert np.all(seq[1] + seq[2] == 20)
+
+
+def test_frame_fault_inside_gather_group_then_renders(rc, scenes):
+    """A failure inside rt_frame_render's RCCL gather group (rt_frame_inject_fault) returns an
+    error with the group closed: the next render on the same frame gathers again and equals a
+    fresh frame's render bit for bit (an open group would swallow its gather)."""
+    scene = scenes["die.txt"]
+    W, H = 64, 40
+    f = rc.GpuFrame(scene, 0, n_gpus=1, size=(W, H))
+    f.inject_fault(1)
+    with pytest.raises(rc.RtError, match="injected fault"):
+        f.render(4, seed=5, sample_base=0)
+    s, n, m, r = f.render(4, seed=5, sample_base=0)
+    f.close()
+    g = rc.GpuFrame(scene, 0, n_gpus=1, size=(W, H))
+    s2, n2, m2, r2 = g.render(4, seed=5, sample_base=0)
+    g.close()
+    assert r == r2 and np.array_equal(n, n2) and np.array_equal(m, m2) and np.array_equal(s, s2)
+    assert np.all(n + m == 4)
 
 
 def test_many_launches_two_streams(rc, scenes):

@@ -412,3 +412,13 @@ def test_host_pool_survives_fork(rc):
         p.kill()
     assert not alive, "forked child hung in the host pool"
     assert p.exitcode == 0 and q.get(timeout=5)
+
+
+def test_library_built_from_these_sources():
+    """The library carries the hash of the sources it was built from (rt_build_info, Makefile +
+    csrc/source_hash.py): it equals the hash of the tree's sources, with no extra compiler flags,
+    so the library every test loads is the committed source's build, not a stale or variant one."""
+    import raytracercore_amd as rc
+    from raytracercore_amd.csrc.source_hash import build_info
+
+    assert rc.load_library().rt_build_info().decode() == build_info("")
