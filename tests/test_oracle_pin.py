@@ -25,6 +25,7 @@ over a few thousand pixels (seeds 1-3: die.png 0.990-1.002, app.png 0.991-1.010)
 * bounce-with-lens.png (1200x1200) was captured at an unknown exposure/recursion setting (its
   linear radiance is ~1.4x the file's recursion-10 render): geometry plus one uniform factor.
 """
+import functools
 import os
 from concurrent.futures import ThreadPoolExecutor
 
@@ -188,17 +189,16 @@ def test_bounce_screenshot_geometry_and_uniform_exposure():
     assert ratios.std() / ratios.mean() < 0.15, ratios
 
 
-# Sphere 13 (bounce.txt:88, diffuse .9 / specular .2 at shininess 250) is the region of app.png
-# nearest the bound: R -3.6 %, G -1.3 %, B -2.4 % beyond the quantisation interval here (1,024 spp,
-# seed 1), -3.9 % R at 3,072 spp.  In mid-interval terms the oracle is ~3.5 % darker in luminance,
-# concentrated on the sphere's upper half.  The reference's silhouette of the sphere aligns with
-# the oracle's at the viewport offset, and the screenshot's own pixel noise there matches
-# ~3,000-7,000 spp, so neither geometry nor screenshot noise explains it; the .NET System.Random
-# draw order (oracle_render_tile_netrandom), recursion and shininess variants do not move it.  It
-# stays within the 4 % bound every region is held to, and is recorded as an open parity item
-# (tools/sphere13_diag.py).
+# app.png's viewport sits at (5, 86) of the window (tests/golden/make_golden.py APP_OFFSET): the
+# light box's saturated footprint pins it to the pixel (test_bounce_app_viewport_offset_from_light_box).
+# Until round 6 the fixture was cut at (4, 85), one pixel off in x and y; that alone put sphere 13
+# (bounce.txt:88) 3.5 % below the screenshot -- -7 to -16 % R in its upper cells, where the one-pixel
+# shift slides its bright rim over the darker shading -- and the ceiling ring around the light box
+# 12 % above it.  At (5, 86) both read within 0.3 % at full resolution (tools/app_offset_diag.py,
+# DESIGN.md §4.1), and every region is held to 2 % instead of 4 %.
 
 
+@functools.lru_cache(maxsize=None)
 def _app_regions(spp, seed=1):
     d = np.load(os.path.join(GOLDEN, "screenshot_app_bounce700.npz"))
     ref, xs, ys = d["rgb"].astype(np.int64), d["xs"], d["ys"]
@@ -212,18 +212,106 @@ def _app_regions(spp, seed=1):
 
 def test_bounce_app_screenshot_exposure1_radiance():
     """bounce.txt at exposure 1.000 (Screenshots/app.png viewport, every 4th pixel): coverage, the
-    per-channel mean linear radiance of the fully covered, unsaturated pixels within 2 % of the
+    per-channel mean linear radiance of the fully covered, unsaturated pixels within 1 % of the
     oracle (1,024 spp), and region by region: every primitive with at least 200 usable pixels --
     the room's walls, floor and ceiling, the cut-out faces, sphere 13, the rotated cube's faces and
-    the Fresnel / TIR lens (20) -- within 4 %."""
+    the Fresnel / TIR lens (20) -- within 2 %."""
     ref, got, lin, panel, ok, rid, inner = _app_regions(1024)
     agree = (panel != (got[..., 3] > 0)).mean()
-    assert agree > 0.985, f"coverage agreement {agree:.4f}"
+    assert agree > 0.995, f"coverage agreement {agree:.4f}"
     assert ok.sum() > 10000
     ratio = _linear_ratio(ref, lin, ok)
     print("app.png exposure-1 radiance ratio (R, G, B):", ratio, "pixels", int(ok.sum()))
-    assert np.all(np.abs(ratio - 1) < 0.02), ratio
+    assert np.all(np.abs(ratio - 1) < 0.01), ratio
     regions = [(int(r), rid == r) for r in range(22)]
-    out = _check_regions("app.png", ref, lin, ok & inner, rid, regions, 0.04)
+    out = _check_regions("app.png", ref, lin, ok & inner, rid, regions, 0.02)
     # the lens, sphere 13, the floor (10), the far walls (6, 9) and a rotated-cube face must be among them
     assert {6, 9, 10, 13, 20} <= set(out) and len(out) >= 8, sorted(out)
+
+
+def _app_crop(key):
+    d = np.load(os.path.join(GOLDEN, "screenshot_app_bounce700.npz"))
+    return d[key].astype(np.int64), tuple(int(v) for v in d[key + "_window"])
+
+
+def _window_mean(x0, y0, w, h, spp, seed=1):
+    """The oracle's linear per-pixel means [h, w, 3] over a window of the 700 x 700 frame."""
+    orc = OracleScene.from_file(os.path.join(GOLDEN, "scenes", "bounce.txt"))
+    orc.set_size(700, 700)
+    out = np.zeros((h, w, 3))
+
+    def row(j):
+        s, n, _, _ = orc.render_tile(x0, y0 + j, w, 1, spp, seed=seed)
+        out[j] = s[:, 0] / np.maximum(n[:, 0], 1)[:, None]
+
+    with ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
+        list(ex.map(row, range(h)))
+    return out
+
+
+def test_bounce_app_viewport_offset_from_light_box():
+    """The light box (bounce.txt:29-32, emission 5) in app.png: its saturated footprint (the box and
+    the ceiling next to it, which it lights above 1) equals the oracle's at the fixture's viewport
+    offset and at no shift within 3 pixels -- the screenshot is registered to the pixel, and the
+    box's position, size and visible faces (+x, -y and the bottom +z, IDs 0, 3, 4) are the
+    reference's."""
+    crop, (x0, y0, w, h) = _app_crop("light")
+    m = 3  # the crop's margin on every side
+    lin = _window_mean(x0 + m, y0 + m, w - 2 * m, h - 2 * m, 512)
+    ours = (np.clip(lin, 0, 1) ** (1 / 2.2) * 255).astype(np.int64).max(-1) >= 250  # GetOutput's truncation
+    diff = {}
+    for dy in range(-m, m + 1):
+        for dx in range(-m, m + 1):
+            sat = crop[m + dy:m + dy + h - 2 * m, m + dx:m + dx + w - 2 * m].max(-1) >= 250
+            diff[(dx, dy)] = int((sat ^ ours).sum())
+    best = min(diff, key=diff.get)
+    print("light box saturated pixels", int(ours.sum()), "differing at shift (0, 0):", diff[(0, 0)],
+          "next best:", sorted(diff.values())[1])
+    assert best == (0, 0) and diff[(0, 0)] <= 0.03 * ours.sum(), diff
+    assert sorted(diff.values())[1] >= 1.5 * diff[(0, 0)] + 10
+    orc = OracleScene.from_file(os.path.join(GOLDEN, "scenes", "bounce.txt"))
+    orc.set_size(700, 700)
+    ids = orc.primary_ids(x0, y0, w, h).T  # [y, x]
+    light = (ids >= 0) & (ids <= 4)
+    assert set(np.unique(ids[light]).tolist()) == {0, 3, 4}
+    # every pixel the box covers whole (its 3 x 3 neighbourhood's corner IDs all on the box; a primary-ID
+    # pixel is sampled at its corner) is saturated in the screenshot
+    from scipy.ndimage import binary_erosion
+
+    whole = binary_erosion(light, np.ones((3, 3), bool))
+    assert whole.sum() > 1500 and (crop[whole].max(-1) >= 250).all()
+
+
+def test_bounce_app_subregions_sphere13_and_ceiling_ring():
+    """Sub-regions that a region average could hide: sphere 13's upper and lower halves
+    (every 4th pixel) and the ceiling ring 2-10 pixels around the light box (full resolution) --
+    the sphere's upper half faces the ceiling and the light, the ring is lit by the box's sides at
+    grazing angles -- each within 2 % of the screenshot, as every region is."""
+    ref, got, lin, panel, ok, rid, inner = _app_regions(1024)
+    d = np.load(os.path.join(GOLDEN, "screenshot_app_bounce700.npz"))
+    ys = d["ys"]
+    usable = ok & inner & (rid == 13) & (ref.max(-1) >= 16)
+    rows = np.nonzero(usable)[0]
+    mid_row = np.median(rows)
+    upper = usable & (np.arange(usable.shape[0])[:, None] < mid_row)  # image up is the scene's -z: the ceiling
+    lower = usable & ~upper
+    print("sphere 13 halves split at screen row", int(ys[int(mid_row)]))
+    out = _check_regions("app.png sphere 13", ref, lin, usable, rid, [("upper", upper), ("lower", lower)], 0.02,
+                         min_pixels=150)
+    assert set(out) == {"upper", "lower"}
+    # the ceiling ring: the ceiling (9) 2-10 pixels from the light box's primary-ID footprint, unsaturated
+    from scipy.ndimage import distance_transform_edt
+
+    crop, (x0, y0, w, h) = _app_crop("ring")
+    orc = OracleScene.from_file(os.path.join(GOLDEN, "scenes", "bounce.txt"))
+    orc.set_size(700, 700)
+    ids = orc.primary_ids(x0, y0, w, h).T
+    dist = distance_transform_edt(~((ids >= 0) & (ids <= 4)))
+    ring = (ids == 9) & (dist >= 2) & (dist <= 10) & (crop.max(-1) < 250)
+    jj, ii = np.nonzero(ring)
+    lin_p, miss_p = _render_points("bounce.txt", (700, 700), list(zip(x0 + ii, y0 + jj)), 512, seed=1)
+    assert (miss_p == 0).all() and len(jj) > 1000
+    lin_r = np.zeros((h, w, 3))
+    lin_r[jj, ii] = lin_p
+    out = _check_regions("app.png ceiling ring", crop, lin_r, ring, ids, [("ring", ring)], 0.02)
+    assert set(out) == {"ring"}
