@@ -427,8 +427,17 @@ BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<
         const double aa = dot_s(a, a), bb = dot_s(b, b);
         return aa > 0 && bb > 0 && dot_s(c, c) <= 1e-18 * aa * bb;
     };
+    // The box and frame finders pair rectangles by search (quadratic in the group's rectangles).
+    // They only make the brute-force orders cheaper to test, and a group with more than
+    // kFindMax candidates belongs to a scene the BVH kernels render (AUTO takes brute force up to 48
+    // primitives), so such a group keeps its rectangles as they are: scene creation stays linear
+    // (8,000 single axis-aligned rectangles took 0.7 s, 100,000 would take minutes).
+    constexpr size_t kFindMax = 4096;
     auto find_frames = [&](const std::vector<int>& ids) {
         std::vector<FrameB> fr;
+        size_t cand = 0;
+        for (int i : ids) cand += kind_of[i] == 3 && (H[i].flags & F_MIRROR) && !(H[i].flags & F_HASNORMALS);
+        if (cand > kFindMax) return fr;
         for (int i : ids) {
             const HostPrim& p = H[i];
             if (kind_of[i] != 3 || !(p.flags & F_MIRROR) || (p.flags & F_HASNORMALS)) continue;
@@ -682,7 +691,7 @@ BruteOrders make_brute_orders(const std::vector<HostPrim>& H, const std::vector<
             for (int i : g)
                 if (kind_of[i] < 3) wr.push_back(rect_geom(i, kind_of[i], nullptr, nullptr));
             std::vector<char> wused(wr.size(), 0);
-            const auto wboxes = use_boxes ? find_boxes(wr, wused) : std::vector<BoxFit>{};
+            const auto wboxes = use_boxes && wr.size() <= kFindMax ? find_boxes(wr, wused) : std::vector<BoxFit>{};
             for (int kind = 0; kind < 3; kind++)
                 for (size_t j = 0; j < wr.size(); j++) {
                     if (wused[j] || wr[j].k != kind) continue;

@@ -422,3 +422,29 @@ def test_library_built_from_these_sources():
     from raytracercore_amd.csrc.source_hash import build_info
 
     assert rc.load_library().rt_build_info().decode() == build_info("")
+
+
+def test_brute_layout_linear_on_large_rectangle_scenes():
+    """The flat brute-force order is built for every scene; its box and frame finders pair
+    rectangles by search, so a group with more than 4,096 candidates keeps its rectangles as they
+    are (rtcore_api.hip kFindMax): 30,000 axis-aligned single faces and 6,000 rotated cube faces lay
+    out in well under a second instead of minutes, while a small scene still finds its boxes."""
+    import time
+
+    import raytracercore_amd as rc
+
+    rng = np.random.default_rng(3)
+    head = "size 64 48\ncamera 0 -8 0, 0 0 0, 0 0 1, 60\ndiffuse .5 .5 .5\n"
+    faces = "".join(f"cube {x:.4f} {y:.4f} {z:.4f} .05 .05 .05 only +x\n" for x, y, z in rng.uniform(-3, 3, (30000, 3)))
+    sc = rc.SceneLoader.from_text(head + faces)
+    t = time.perf_counter()
+    lay = rc.brute_layout(sc.prims)
+    assert time.perf_counter() - t < 3.0 and lay["rects"] == 30000 and lay["boxes"] == 0
+    rot = "".join(f"pushtransform\ntranslate {x:.3f} {y:.3f} {z:.3f}\nrotate 0 0 1 {a:.2f}\ncube 0 0 0 .05 .05 .05 all\n"
+                  "poptransform\n" for x, y, z, a in np.c_[rng.uniform(-3, 3, (1000, 3)), rng.uniform(1, 89, 1000)])
+    sc = rc.SceneLoader.from_text(head + rot)
+    t = time.perf_counter()
+    lay = rc.brute_layout(sc.prims)
+    assert time.perf_counter() - t < 3.0 and lay["frames"] == 0 and lay["tris"] == 6000
+    small = rc.SceneLoader.from_text(head + "cube 0 0 0 1 1 1 all\ncube 2 0 0 1 1 1 all\n")
+    assert rc.brute_layout(small.prims)["boxes"] == 2
