@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _declared_functions():
     text = open(os.path.join(ROOT, "include", "rtcore.h")).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:int|void|int32_t)\s+(rt_\w+)\s*\(", text, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|int32_t|const char\s*\*)\s*(rt_\w+)\s*\(", text, flags=re.M)))
 
 
 def test_library_exports_every_declared_symbol(rc):
@@ -448,3 +448,19 @@ def test_brute_layout_linear_on_large_rectangle_scenes():
     assert time.perf_counter() - t < 3.0 and lay["frames"] == 0 and lay["tris"] == 6000
     small = rc.SceneLoader.from_text(head + "cube 0 0 0 1 1 1 all\ncube 2 0 0 1 1 1 all\n")
     assert rc.brute_layout(small.prims)["boxes"] == 2
+
+
+def test_scene_create_refuses_frames_past_16_bit_coordinates(rc):
+    """The BVH kernels hold a pixel's x and y in 16 bits each (kernels_path.hip lane_fx / lane_fy):
+    rt_scene_create refuses a width or height above 65535 with RT_ERR_ARG and a message, before it
+    touches a device (so this runs without one)."""
+    lib = rc.load_library()
+    sc = rc.SceneLoader.from_text(SYNTH)
+    for w, h in ((65536, 16), (16, 70000)):
+        params = rc.rt_scene_params.from_buffer_copy(sc.params)
+        params.width, params.height = w, h
+        handle = C.c_void_p()
+        assert lib.rt_scene_create(C.byref(params), sc.prims, sc.n_prims, 0, C.byref(handle)) == -1
+        buf = C.create_string_buffer(256)
+        lib.rt_last_error(buf, 256)
+        assert b"65535" in buf.value and not handle.value
