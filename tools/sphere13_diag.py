@@ -1,7 +1,9 @@
 """Sphere 13 of app.png against the oracle, pixel group by pixel group (CPU only, diagnostic).
 
-VERDICT r4 item 1: sphere 13 (bounce.txt:88) reads 3-4 % darker in the oracle than in the
-reference's own screenshot while the cut-out face 11 next to it reads 1.4-2.1 % brighter.  This
+VERDICT r4 item 1: sphere 13 (bounce.txt:88) read 3-4 % darker in the oracle than in the
+reference's own screenshot while the cut-out face 11 next to it read 1.4-2.1 % brighter.  Round 6
+found the cause: the fixture had been cut one pixel off (tools/app_offset_diag.py); with the
+fixture at its registered offset (5, 86) this tool reads sphere 13 within noise.  This
 splits the sphere's usable pixels by the direction of the surface normal at the primary hit and
 prints, per bin, oracle / screenshot in linear radiance (the screenshot linearised at the middle
 of its 8-bit truncation interval, as tests/test_oracle_pin.py does).
