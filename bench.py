@@ -320,8 +320,8 @@ def launch_ranks(args_list, n: int) -> int:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="bounce1080", choices=sorted(CONFIGS))
     ap.add_argument("--spp", type=int, default=0, help="override samples per pixel per step")
     ap.add_argument("--traversal", default="auto", choices=["auto", "brute", "bvh", "bvh2", "grouped"])
