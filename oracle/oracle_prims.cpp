@@ -22,7 +22,7 @@ V4 Prim::get_center() const
 {
     switch (kind) {
     case kTri: return (vp[0] + vp[1] + vp[2]) / 3; // Triangle.cs:226-229
-    case kSphere: return transformed ? mvmul(to_obj, center) : center; // Sphere.cs:521-527
+    case kSphere: return transformed ? mvmul(to_obj, center) : center; // Sphere.cs:212-218
     default: return v4(0, 0, 0, 1) + pnormal * origin_dist; // Plane.cs:24-27
     }
 }
@@ -42,7 +42,7 @@ double Prim::max_center_distance(V4 dir) const
         if (!eq3(v3, v4(0, 0, 0, 0))) dist = net_max(f(v3), dist);
         return dist;
     }
-    if (kind == kSphere) { // Sphere.cs:529-541
+    if (kind == kSphere) { // Sphere.cs:220-232
         if (transformed) {
             double s = std::sqrt(1 - dir.x * dir.x);
             V4 vec = v4(dir.x, dir.y * s, dir.z * s, 0);

@@ -35,7 +35,7 @@ double box_sa(const Box& b) { return ((b.size.x * b.size.y) + (b.size.y * b.size
 
 static Vec4d from(const rt_vec4d& v) { return Vec4d{v.x, v.y, v.z, v.w}; }
 
-// IBoundedObject.GetCenter (Triangle.cs:226-229, Sphere.cs:521-527, Plane.cs:24-27)
+// IBoundedObject.GetCenter (Triangle.cs:226-229, Sphere.cs:212-218, Plane.cs:24-27)
 static Vec4d prim_center(const HostPrim& p)
 {
     switch (p.kind) {
@@ -45,7 +45,7 @@ static Vec4d prim_center(const HostPrim& p)
     }
 }
 
-// IBoundedObject.GetMaxCenterDistance (Triangle.cs:231-263, Sphere.cs:529-541, Plane.cs:68-74)
+// IBoundedObject.GetMaxCenterDistance (Triangle.cs:231-263, Sphere.cs:220-232, Plane.cs:68-74)
 static double prim_extent(const HostPrim& p, Vec4d dir)
 {
     if (p.kind == RT_PRIM_TRIANGLE) {
