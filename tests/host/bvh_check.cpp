@@ -6,7 +6,10 @@
 //   * have, for every wide node, dequantised child planes (origin + q * 2^e, in exact
 //     arithmetic) that contain every primitive box below that child;
 //   * never need more traversal-stack entries than the computed stack_need.
-// Prints "ok <n_prims> <bvh2 nodes> <wide nodes> <stack_need>" per collapse or the first failure.
+// Prints "ok <n_prims> <bvh2 nodes> <wide nodes> <stack_need>" per collapse or the first failure;
+// with --ref also builds the reference BVH and the cameras (the host inputs of the exact pass).
+// `make bvh_check_asan` builds it with AddressSanitizer and UndefinedBehaviorSanitizer on the host
+// sources (tests/test_host.py runs both builds).
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -153,6 +156,15 @@ int main(int argc, char** argv)
             return 1;
         }
         std::printf("%s %zu %zu %zu %d\n", mode ? "" : "ok", H.size(), b2.nodes.size(), b4.nodes.size(), b4.stack_need);
+    }
+    if (argc > 2 && std::strcmp(argv[2], "--ref") == 0) { // the exact pass's inputs too (sanitizer runs)
+        const RefBvh r = build_ref_bvh(H);
+        for (const rt_camera& cam : ps.cameras) {
+            CameraD d;
+            CameraF cf;
+            camera_init(cam, ps.params.width, ps.params.height, d, cf);
+        }
+        std::printf("ref %zu %d\n", r.nodes.size(), r.depth);
     }
     return 0;
 }
