@@ -41,6 +41,19 @@ KASM(k_med3_vvv, "v_med3_f32 %0, %1, %2, %0", "+v"(x[i]) : "v"(bv), "v"(cv))
 KASM(k_pkfma_vvv, "v_pk_fma_f32 %0, %1, %2, %0", "+v"(*(double*)&x[i & ~1]) : "v"(*(double*)&x[(i + 2) & 15]), "v"(*(double*)&x[(i + 4) & 15]))
 KASM(k_pkadd_vv, "v_pk_add_f32 %0, %1, %0", "+v"(*(double*)&x[i & ~1]) : "v"(*(double*)&x[(i + 2) & 15]))
 KASM(k_mov_sv, "v_mov_b32_e32 %0, %1", "=v"(x[i]) : "s"(a))
+// round 6: forms a quantised-node slab test could use instead of v_cvt_f32_ubyte + v_fma
+KASM(k_cvt_ubyte1, "v_cvt_f32_ubyte1_e32 %0, %0", "+v"(x[i]))
+KASM(k_mov_sdwa_byte, "v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2", "+v"(x[i]) : "v"(bv))
+KASM(k_mul_u24_sdwa, "v_mul_u32_u24_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD", "+v"(x[i]) : "v"(bv))
+KASM(k_fma_mix, "v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]", "+v"(x[i]) : "v"(bv), "v"(cv))
+KASM(k_fma_mix_hi, "v_fma_mix_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,0,0]", "+v"(x[i]) : "v"(bv), "v"(cv))
+KASM(k_pk_fma_f16, "v_pk_fma_f16 %0, %1, %2, %0", "+v"(x[i]) : "v"(bv), "v"(cv))
+KASM(k_perm, "v_perm_b32 %0, %0, %1, %2", "+v"(x[i]) : "v"(bv), "v"(cv))
+KASM(k_max_u32, "v_max_u32_e32 %0, %0, %1", "+v"(x[i]) : "v"(bv))
+KASM(k_max3_u32, "v_max3_u32 %0, %0, %1, %2", "+v"(x[i]) : "v"(bv), "v"(cv))
+KASM(k_cvt_pk_fp8, "v_cvt_pk_f32_fp8_e32 %0, %1", "+v"(*(double*)&x[i & ~1]) : "v"(bv))
+KASM(k_bfi, "v_bfi_b32 %0, %0, %1, %2", "+v"(x[i]) : "v"(bv), "v"(cv))
+KASM(k_and_vv, "v_and_b32_e32 %0, 3, %0", "+v"(x[i]))
 
 KASM(k_mullo_u32, "v_mul_lo_u32 %0, %0, %1", "+v"(x[i]) : "v"(bv))
 KASM(k_mulhi_u32, "v_mul_hi_u32 %0, %0, %1", "+v"(x[i]) : "v"(bv))
@@ -137,5 +150,17 @@ int main()
     RUN(k_dot2);
     RUN(k_cmpx);
     RUN(k_mov_sv);
+    RUN(k_cvt_ubyte1);
+    RUN(k_mov_sdwa_byte);
+    RUN(k_mul_u24_sdwa);
+    RUN(k_fma_mix);
+    RUN(k_fma_mix_hi);
+    RUN(k_pk_fma_f16);
+    RUN(k_perm);
+    RUN(k_max_u32);
+    RUN(k_max3_u32);
+    RUN(k_cvt_pk_fp8);
+    RUN(k_bfi);
+    RUN(k_and_vv);
     return 0;
 }
