@@ -24,6 +24,9 @@ TRACE_CALL = ("            trace_brute<CULL, STATS>(sc, groups, tests, rects, fr
 BOUNCE_CALL = "            bounce<VN>(L, S, sc, R, vnormals, tests, pq->prims_d, b);\n"
 RAYS_LINE = "        wave_rays += (unsigned)__popcll(__ballot(L.live)); // one Scene.RayTrace per live lane\n"
 
+NODE_LOAD = '                    const Node4Q q = (ref & RT_HOT_BIT) ? lds_hot[ref & ~RT_HOT_BIT] : Node4Q(nodes4[ref]);\n'
+HOT_ON = '    static const bool on = !(getenv("RTCORE_HOT_NODES") && getenv("RTCORE_HOT_NODES")[0] == \'0\'); // A/B switch\n'
+
 PATCHES = {
     # every camera ray misses: the per-sample overhead alone
     "NO_TRACE": [(TRACE_CALL, "")],
@@ -100,6 +103,81 @@ PATCHES = {
                   "                        q.d = make_float4(a3.x, a3.y, a3.z, a3.w);\n"
                   "                    }\n"
                   "                    [[maybe_unused]] const int sp0 = sp;\n")],
+    # round 6, C4 visit VALU: no hot-node table (no LDS-or-global select per visit)
+    "WIDE_NOHOT": [(NODE_LOAD, "                    const Node4Q q = nodes4[ref];\n"),
+                   (HOT_ON, "    static const bool on = false;\n")],
+    # ... and the node read through a buffer resource with a 32-bit byte offset (no 64-bit address math)
+    "WIDE_BUFLOAD": [(NODE_LOAD,
+                      "                    Node4Q q;\n"
+                      "                    {\n"
+                      "                        typedef float v4f __attribute__((ext_vector_type(4)));\n"
+                      "                        const __amdgpu_buffer_rsrc_t rs =\n"
+                      "                            __builtin_amdgcn_make_buffer_rsrc((void*)pq->nodes4, (short)0, -1, 0x00020000);\n"
+                      "                        const unsigned off = (unsigned)ref << 6;\n"
+                      "                        const v4f a0 = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);\n"
+                      "                        const v4f a1 = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0);\n"
+                      "                        const v4f a2 = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 32, 0, 0);\n"
+                      "                        const v4f a3 = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 48, 0, 0);\n"
+                      "                        q.a = make_float4(a0.x, a0.y, a0.z, a0.w);\n"
+                      "                        q.b = make_float4(a1.x, a1.y, a1.z, a1.w);\n"
+                      "                        q.c = make_float4(a2.x, a2.y, a2.z, a2.w);\n"
+                      "                        q.d = make_float4(a3.x, a3.y, a3.z, a3.w);\n"
+                      "                    }\n"),
+                     (HOT_ON, "    static const bool on = false;\n")],
+    # the buffer-resource node read with the hot-node table kept (LDS for the top of the tree)
+    "WIDE_BUFLOAD_HOT": [(NODE_LOAD,
+                          "                    Node4Q q;\n"
+                          "                    if (ref & RT_HOT_BIT) q = lds_hot[ref & ~RT_HOT_BIT];\n"
+                          "                    else {\n"
+                          "                        typedef float v4f __attribute__((ext_vector_type(4)));\n"
+                          "                        const __amdgpu_buffer_rsrc_t rs =\n"
+                          "                            __builtin_amdgcn_make_buffer_rsrc((void*)pq->nodes4, (short)0, -1, 0x00020000);\n"
+                          "                        const unsigned off = (unsigned)ref << 6;\n"
+                          "                        const v4f a0 = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);\n"
+                          "                        const v4f a1 = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0);\n"
+                          "                        const v4f a2 = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 32, 0, 0);\n"
+                          "                        const v4f a3 = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 48, 0, 0);\n"
+                          "                        q.a = make_float4(a0.x, a0.y, a0.z, a0.w);\n"
+                          "                        q.b = make_float4(a1.x, a1.y, a1.z, a1.w);\n"
+                          "                        q.c = make_float4(a2.x, a2.y, a2.z, a2.w);\n"
+                          "                        q.d = make_float4(a3.x, a3.y, a3.z, a3.w);\n"
+                          "                    }\n")],
+    # the leaf step's rows through a buffer resource too (32-bit byte offsets)
+    "LEAF_BUFLOAD": [("        r[j][0] = rows[3 * (k + j)];\n"
+                      "        r[j][1] = rows[3 * (k + j) + 1];\n"
+                      "        r[j][2] = rows[3 * (k + j) + 2];\n",
+                      "        {\n"
+                      "            typedef float v4f __attribute__((ext_vector_type(4)));\n"
+                      "            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)rows, (short)0, -1, 0x00020000);\n"
+                      "            const unsigned off = (unsigned)(k + j) * 48u;\n"
+                      "            const v4f a0 = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);\n"
+                      "            const v4f a1 = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0);\n"
+                      "            const v4f a2 = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 32, 0, 0);\n"
+                      "            r[j][0] = make_float4(a0.x, a0.y, a0.z, a0.w);\n"
+                      "            r[j][1] = make_float4(a1.x, a1.y, a1.z, a1.w);\n"
+                      "            r[j][2] = make_float4(a2.x, a2.y, a2.z, a2.w);\n"
+                      "        }\n")],
+    # the 4-child sort without its last exchange (the two middle pushes in either order)
+    "WIDE_SORT4": [("    cswap(d1, r1, d2, r2);\n", "")],
+    # the direction's signs computed once per query (after the shading phase) instead of per visit
+    "WIDE_SIGNS": [("                                           const TravStack& stk, bool& pop)\n",
+                    "                                           const TravStack& stk, bool& pop, bool sgx, bool sgy, bool sgz)\n"),
+                   ("    const uint32_t nx = id.x >= 0.0f ? lx : hx, fx = id.x >= 0.0f ? hx : lx;\n"
+                    "    const uint32_t ny = id.y >= 0.0f ? ly : hy, fy = id.y >= 0.0f ? hy : ly;\n"
+                    "    const uint32_t nz = id.z >= 0.0f ? lz : hz, fz = id.z >= 0.0f ? hz : lz;\n",
+                    "    const uint32_t nx = sgx ? lx : hx, fx = sgx ? hx : lx;\n"
+                    "    const uint32_t ny = sgy ? ly : hy, fy = sgy ? hy : ly;\n"
+                    "    const uint32_t nz = sgz ? lz : hz, fz = sgz ? hz : lz;\n"),
+                   ("    V3 id{0, 0, 0};\n    Best b{", "    V3 id{0, 0, 0};\n    bool sgx = true, sgy = true, sgz = true;\n    Best b{"),
+                   ("            id = v3(slab_rcp(S.d.x), slab_rcp(S.d.y), slab_rcp(S.d.z));\n",
+                    "            id = v3(slab_rcp(S.d.x), slab_rcp(S.d.y), slab_rcp(S.d.z));\n"
+                    "            sgx = id.x >= 0.0f;\n            sgy = id.y >= 0.0f;\n            sgz = id.z >= 0.0f;\n"),
+                   ("                    wide_visit<STACK>(q, id, oi, b.t, ref, sp, stk, pop);\n",
+                    "                    wide_visit<STACK>(q, id, oi, b.t, ref, sp, stk, pop, sgx, sgy, sgz);\n"),
+                   ("                wide_visit<STACK>(q, id, S.o * id, b.t, ref, sp, stk, pop);\n",
+                    "                wide_visit<STACK>(q, id, S.o * id, b.t, ref, sp, stk, pop, id.x >= 0.0f, id.y >= 0.0f, id.z >= 0.0f);\n"),
+                   ("                wide_visit<STACK>(q, id, oi, b.t, ref, sp, stk, pop);\n",
+                    "                wide_visit<STACK>(q, id, oi, b.t, ref, sp, stk, pop, id.x >= 0.0f, id.y >= 0.0f, id.z >= 0.0f);\n")],
     # no literal folding of zero scene fields in the specialised build
     "NO_KFOLD": [("    return __builtin_constant_p(c) && c == 0.0f;\n", "    return false;\n")],
 }
@@ -130,7 +208,7 @@ def main() -> None:
     tree = os.path.join(out, "tree")
     shutil.rmtree(tree, ignore_errors=True)
     shutil.copytree(os.path.join(ROOT, "include"), os.path.join(tree, "include"))
-    dst = os.path.join(tree, "pkg", "csrc")
+    dst = os.path.join(tree, "raytracercore_amd", "csrc")  # the repository's layout (source_hash.py)
     shutil.copytree(CSRC, dst, ignore=shutil.ignore_patterns("_obj*"))
     kp = os.path.join(dst, "kernels_path.hip")
     with open(kp) as f:
