@@ -25,7 +25,7 @@ def _built():
     orc = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
     if not os.path.exists(orc):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "-j8"], check=True)
-    if not os.path.exists(lib):
+    if not os.path.exists(lib) or not os.path.exists(os.path.join(ROOT, "raytracercore_amd", "worker_host")):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "raytracercore_amd", "csrc"), "-j8"], check=True)
     yield
 
