@@ -21,7 +21,10 @@
 //         holding the same tile may finish its passes out of order);
 //   bulk: counts exactly, Σ to 1e-5 relative (a launch sums a pixel's samples in fp32 chunks
 //         whose size follows the launch's shape, so tile and frame group them differently).
-// usage: worker_host SCENE W H THREADS PASSES MODE(1spp|bulk) SPP [DEVICES]
+// MODE frame is the whole-frame loop of INTEGRATION.md §3 instead: one rt_frame over DEVICES
+// devices (band sets, RCCL gather to device 0), passes submitted one ahead of their collect
+// (rt_frame_submit / rt_frame_collect) and merged in bulk; checked like bulk (THREADS unused).
+// usage: worker_host SCENE W H THREADS PASSES MODE(1spp|bulk|frame) SPP [DEVICES]
 // Prints "ok ..." with the rates, or "FAIL ..." and exits non-zero.
 #include <algorithm>
 #include <atomic>
@@ -272,11 +275,12 @@ int fail(const char* what, int rc = -1)
 int main(int argc, char** argv)
 {
     if (argc < 8) {
-        std::printf("usage: worker_host SCENE W H THREADS PASSES MODE(1spp|bulk) SPP [DEVICES]\n");
+        std::printf("usage: worker_host SCENE W H THREADS PASSES MODE(1spp|bulk|frame) SPP [DEVICES]\n");
         return 2;
     }
     const int W = std::atoi(argv[2]), H = std::atoi(argv[3]), T = std::atoi(argv[4]), P = std::atoi(argv[5]);
-    const bool bulk = std::strcmp(argv[6], "bulk") == 0;
+    const bool frame_mode = std::strcmp(argv[6], "frame") == 0;
+    const bool bulk = frame_mode || std::strcmp(argv[6], "bulk") == 0;
     const int spp = bulk ? std::atoi(argv[7]) : 1;
     int devices = rt_device_count();
     if (argc > 8) devices = std::min(devices, std::atoi(argv[8]));
@@ -297,28 +301,71 @@ int main(int argc, char** argv)
     params.height = H;
     const uint64_t seed = 0x5eed5eedULL;
 
-    // --- the threaded host: T workers, one scene handle each, devices round-robin ---
+    const size_t N = (size_t)W * H;
     Owner owner(W, H, T, P, bulk);
-    std::vector<Worker*> workers;
-    for (int i = 0; i < T; i++) workers.push_back(new Worker(owner, params, prims, cams[0], i % devices, seed, bulk, spp));
-    if (g_failed) return 1;
-    owner.set_workers(T);
-    const auto t0 = std::chrono::steady_clock::now();
-    std::vector<std::thread> threads;
-    for (Worker* w : workers) threads.emplace_back([w] { w->render(); });
-    owner.update_loop();
-    for (auto& t : threads) t.join();
-    const double host_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    for (Worker* w : workers) delete w;
-    if (g_failed) return 1;
-    if (owner.merged_passes() != (uint64_t)P * owner.tile_count()) return fail("not every pass was merged");
+    std::vector<rt_color> frame_sum;
+    std::vector<uint32_t> frame_samples, frame_misses;
+    uint64_t frame_rays = 0;
+    double host_s = 0.0;
+    if (!frame_mode) {
+        // --- the threaded host: T workers, one scene handle each, devices round-robin ---
+        std::vector<Worker*> workers;
+        for (int i = 0; i < T; i++)
+            workers.push_back(new Worker(owner, params, prims, cams[0], i % devices, seed, bulk, spp));
+        if (g_failed) return 1;
+        owner.set_workers(T);
+        const auto t0 = std::chrono::steady_clock::now();
+        std::vector<std::thread> threads;
+        for (Worker* w : workers) threads.emplace_back([w] { w->render(); });
+        owner.update_loop();
+        for (auto& t : threads) t.join();
+        host_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        for (Worker* w : workers) delete w;
+        if (g_failed) return 1;
+        if (owner.merged_passes() != (uint64_t)P * owner.tile_count()) return fail("not every pass was merged");
+    } else {
+        // --- the whole-frame loop: submit one pass ahead, collect, merge in bulk ---
+        rt_frame* fr = nullptr;
+        rc = rt_frame_create(&params, prims.data(), n, &cams[0], devices, &fr);
+        if (rc != 0) return fail("rt_frame_create", rc);
+        frame_sum.assign(N, rt_color{0, 0, 0});
+        frame_samples.assign(N, 0);
+        frame_misses.assign(N, 0);
+        std::vector<rt_color> s(N);
+        std::vector<uint32_t> ns(N), ms(N);
+        const auto t0 = std::chrono::steady_clock::now();
+        rc = rt_frame_submit(fr, spp, seed, 0);
+        for (int k = 0; k < P && rc == 0; k++) {
+            if (k + 1 < P) rc = rt_frame_submit(fr, spp, seed, (uint64_t)(k + 1) * spp); // next pass renders...
+            if (rc != 0) break;
+            std::fill(s.begin(), s.end(), rt_color{0, 0, 0}); // collect adds into its buffers
+            std::fill(ns.begin(), ns.end(), 0u);
+            std::fill(ms.begin(), ms.end(), 0u);
+            uint64_t rays = 0;
+            rc = rt_frame_collect(fr, s.data(), ns.data(), ms.data(), &rays); // ...while this one merges
+            for (size_t i = 0; rc == 0 && i < N; i++) {
+                frame_sum[i].r += s[i].r;
+                frame_sum[i].g += s[i].g;
+                frame_sum[i].b += s[i].b;
+                frame_samples[i] += ns[i];
+                frame_misses[i] += ms[i];
+            }
+            frame_rays += rays;
+        }
+        host_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        rt_frame_destroy(fr);
+        if (rc != 0) return fail("rt_frame_submit / rt_frame_collect", rc);
+    }
+    const std::vector<rt_color>& got_sum = frame_mode ? frame_sum : owner.sum();
+    const std::vector<uint32_t>& got_samples = frame_mode ? frame_samples : owner.samples();
+    const std::vector<uint32_t>& got_misses = frame_mode ? frame_misses : owner.misses();
+    const uint64_t got_rays = frame_mode ? frame_rays : owner.rays();
 
     // --- the reference: one handle, whole-frame renders of the same sample indices, merged in order ---
     rt_scene* ref = nullptr;
     rc = rt_scene_create(&params, prims.data(), n, 0, &ref);
     if (rc == 0) rc = rt_scene_set_camera(ref, &cams[0]);
     if (rc != 0) return fail("reference scene", rc);
-    const size_t N = (size_t)W * H;
     std::vector<rt_color> rsum(N, rt_color{0, 0, 0});
     std::vector<uint32_t> rsam(N, 0), rmis(N, 0);
     uint64_t rrays = 0;
@@ -376,14 +423,14 @@ int main(int argc, char** argv)
     uint64_t total_samples = 0, total_misses = 0;
     double worst = 0.0;
     for (size_t i = 0; i < N; i++) {
-        if (owner.samples()[i] != rsam[i] || owner.misses()[i] != rmis[i]) {
-            std::printf("FAIL counts at pixel x=%zu y=%zu: %u/%u against %u/%u\n", i / H, i % H, owner.samples()[i],
-                        owner.misses()[i], rsam[i], rmis[i]);
+        if (got_samples[i] != rsam[i] || got_misses[i] != rmis[i]) {
+            std::printf("FAIL counts at pixel x=%zu y=%zu: %u/%u against %u/%u\n", i / H, i % H, got_samples[i],
+                        got_misses[i], rsam[i], rmis[i]);
             return 1;
         }
         total_samples += rsam[i];
         total_misses += rmis[i];
-        const double a[3] = {owner.sum()[i].r, owner.sum()[i].g, owner.sum()[i].b};
+        const double a[3] = {got_sum[i].r, got_sum[i].g, got_sum[i].b};
         const double b[3] = {rsum[i].r, rsum[i].g, rsum[i].b};
         for (int c = 0; c < 3; c++) {
             if (!std::isfinite(a[c])) return fail("non-finite Σ");
@@ -395,14 +442,14 @@ int main(int argc, char** argv)
         return 1;
     }
     if (total_samples + total_misses != (uint64_t)N * P * spp) return fail("samples + misses != pixels x passes x spp");
-    if (bulk && owner.rays() != rrays) {
-        std::printf("FAIL rays %llu against %llu\n", (unsigned long long)owner.rays(), (unsigned long long)rrays);
+    if (bulk && got_rays != rrays) {
+        std::printf("FAIL rays %llu against %llu\n", (unsigned long long)got_rays, (unsigned long long)rrays);
         return 1;
     }
     const double msps = (double)N * P * spp / host_s * 1e-6;
     std::printf("ok %s %dx%d threads %d tiles %zu passes %d mode %s spp %d devices %d: samples %llu misses %llu "
                 "worst %.3g; workers %.3f s (%.1f M samples/s incl. merge), one handle %.3f s\n",
-                argv[1], W, H, T, owner.tile_count(), P, bulk ? "bulk" : "1spp", spp, devices,
+                argv[1], W, H, T, owner.tile_count(), P, argv[6], spp, devices,
                 (unsigned long long)total_samples, (unsigned long long)total_misses, worst, host_s, msps, ref_s);
     return 0;
 }
