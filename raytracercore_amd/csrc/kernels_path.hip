@@ -1065,6 +1065,15 @@ __device__ __forceinline__ int lane_fy(const Lane& L)
 {
     return NT ? (int)((unsigned)L.fx >> 16) : L.fy;
 }
+// The next sample of the lane's item.  The BVH (NT) kernels hold no register for it: the item's
+// first sample (its chunk, from the item index) plus the samples it finished (samples + misses).
+template <bool NT, class ParT>
+__device__ __forceinline__ int item_sample(const Lane& L, const ParT& p)
+{
+    if (!NT) return L.s_next;
+    const int c = (int)((L.item >> 6) & (unsigned)(p.n_chunks - 1));
+    return c * p.chunk + (int)(L.cnt & 0xFFu) + (int)((L.cnt >> 8) & 0xFFu);
+}
 template <bool NT, class ParT, class SceneT, class CamT>
 __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const SceneT& s, const CamT& cam, int lane,
                                       unsigned total)
@@ -1126,8 +1135,9 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
                 const int px = (int)bx * 8 + (q & 7), py = (int)by * 8 + (q >> 3);
                 if (px < p.w && py < p.h && c * p.chunk < p.spp) {
                     L.item_open = true;
-                    L.s_next = c * p.chunk;
-                    L.cnt = (unsigned)(min(p.spp, L.s_next + p.chunk) - L.s_next) << 16; // chunk <= 64
+                    const int s0 = c * p.chunk;
+                    if (!NT) L.s_next = s0; // (the BVH kernels derive it: item_sample)
+                    L.cnt = (unsigned)(min(p.spp, s0 + p.chunk) - s0) << 16; // chunk <= 64
                     L.ar = L.ag = L.ab = 0.0f;
                     L.fx = p.x0 + px;
                     L.fy = p.y0 + py;
@@ -1164,7 +1174,7 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
         if (NT) // the key from the pixel at every sample start: two registers fewer held
             L.pkey = rt_rng_pixel_key(p.seed_key, (unsigned long long)lane_fy<NT>(L) * (unsigned long long)p.scene.width +
                                                       (unsigned long long)lane_fx<NT>(L));
-        S.rng = rt_rng_from_pixel_key(L.pkey, p.sample_base + (unsigned long long)L.s_next);
+        S.rng = rt_rng_from_pixel_key(L.pkey, p.sample_base + (unsigned long long)item_sample<NT>(L, p));
         start_sample<!NT>(cam, lane_fx<NT>(L), lane_fy<NT>(L), S);
         L.live = true;
     }
@@ -1183,19 +1193,19 @@ __device__ __forceinline__ void bounce(Lane& L, Sample& S, const SceneT& s, cons
         L.ag += hit ? col.y : 0.0f;
         L.ab += hit ? col.z : 0.0f;
         L.cnt += hit ? 1u - 65536u : 256u - 65536u; // one more sample or miss, one fewer left
-        L.s_next++;
+        if (!SLOT) L.s_next++; // (the BVH kernels derive it from cnt: item_sample)
         L.live = false;
         if (!SLOT) {
             // The sample is over: its ray state is dead until the next start_sample writes all of it.
             // Saying so (an empty asm that "defines" the registers) lets the register allocator give
             // these values the registers the continuing lanes' new ray state takes, instead of
-            // copying the 13 sample registers out and back at this divergent join (23 moves per
+            // copying the 12 sample registers out and back at this divergent join (23 moves per
             // iteration in the bounce.txt listing; measured: C2 unchanged, C3 27.31-27.40 ->
             // 27.25-27.31 ms).  The BVH kernels, whose finished lanes wait for the batched shading
             // phase, keep the plain form.
             asm volatile("" : "=v"(S.o.x), "=v"(S.o.y), "=v"(S.o.z), "=v"(S.d.x), "=v"(S.d.y), "=v"(S.d.z),
                          "=v"(S.tint.x), "=v"(S.tint.y), "=v"(S.tint.z), "=v"(S.bounce), "=v"(S.prev),
-                         "=v"(S.rng.k0), "=v"(S.rng.k1));
+                         "=v"(S.rng.x));
         }
     }
 }

@@ -165,9 +165,14 @@ def _spec_draws(seed, pixel, sample, n):
     s1 = _h32((seed >> 32) ^ 0x85EBCA6B ^ s0)
     p0 = _h32((pixel & m) ^ s0)
     p1 = _h32((pixel >> 32) + p0 + s1)
-    k0 = _h32((sample & m) ^ p0)
-    k1 = _h32((sample >> 32) + k0 + p1)
-    return [(_h32(((k0 + i * 0x9E3779B9) & m) ^ k1) >> 8) * 2.0 ** -24 for i in range(n)]
+    x = (_h32((sample & m) ^ p0) ^ ((p1 + (sample >> 32) * 0x9E3779B9) & m)) | 1
+    out = []
+    for _ in range(n):  # xorshift32 (13, 17, 5)
+        x ^= (x << 13) & m
+        x ^= x >> 17
+        x ^= (x << 5) & m
+        out.append((x >> 8) * 2.0 ** -24)
+    return out
 
 
 @pytest.mark.parametrize("seed,pixel,sample", [(0, 0, 0), (1, 12345, 7), (2**40 + 3, 2**33 + 5, 2**35 + 11)])
@@ -191,3 +196,24 @@ def test_rng_statistics():
     for a, b in [(d[:, :-1].ravel(), d[:, 1:].ravel()), (d[:-1].ravel(), d[1:].ravel())]:
         assert abs(np.corrcoef(a, b)[0, 1]) < 0.02
     assert abs(u.mean() - 0.5) < 0.005
+
+
+def test_rng_pairs_and_lags():
+    """The xorshift32 stream's consecutive draws are used as 2-D points (theta with the pow draw,
+    the camera's sub-pixel x and y, the diffuse acos and angle): 16x16 chi-square of (U_n, U_n+1)
+    at every draw index a path reaches, correlations at lags 1-4, and the first draws of
+    neighbouring pixels and samples."""
+    from oracle.oracle import rng_draws
+
+    d = np.array([rng_draws(3, px, s, 24) for px in range(8) for s in range(1500)])
+    for j in range(0, 23, 2):
+        h = np.histogram2d(d[:, j], d[:, j + 1], bins=16, range=[[0, 1], [0, 1]])[0]
+        exp = d.shape[0] / 256
+        chi2 = ((h - exp) ** 2 / exp).sum()
+        assert chi2 < 360, (j, chi2)  # 255 dof: p ~ 1e-5
+    for lag in range(1, 5):
+        assert abs(np.corrcoef(d[:, :-lag].ravel(), d[:, lag:].ravel())[0, 1]) < 0.01
+    # the same sample index of neighbouring pixels, and neighbouring samples of one pixel
+    first = d[:, :2].reshape(8, 1500, 2)
+    assert abs(np.corrcoef(first[:-1, :, 0].ravel(), first[1:, :, 0].ravel())[0, 1]) < 0.02
+    assert abs(np.corrcoef(first[:, :-1, 1].ravel(), first[:, 1:, 1].ravel())[0, 1]) < 0.02

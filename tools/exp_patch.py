@@ -34,7 +34,7 @@ PATCHES = {
     "DUP_SHADE": [(BOUNCE_CALL,
                    "            {\n"
                    "                Sample S2 = S;\n"
-                   "                S2.rng.k0 ^= (unsigned)S.bounce;\n"
+                   "                S2.rng.x ^= (unsigned)S.bounce;\n"
                    "                V3 c2;\n"
                    "                shade<VN>(sc, R.prims, R.mats, R.xfs, vnormals, tests, pq->prims_d, b, S2, c2);\n"
                    "                if (c2.x + S2.d.x == 1234.5f) pq->partial[0].x = 1.0f;\n"
@@ -43,7 +43,7 @@ PATCHES = {
     "DUP_START": [(RAYS_LINE,
                    "        if (L.live) {\n"
                    "            Sample S2 = S;\n"
-                   "            S2.rng.k0 ^= (unsigned)S.bounce;\n"
+                   "            S2.rng.x ^= (unsigned)S.bounce;\n"
                    "            start_sample<true>(*cp, L.fx, L.fy, S2);\n"
                    "            if (S2.o.x + S2.d.y == 1234.5f) pq->partial[0].x = 1.0f;\n"
                    "        }\n" + RAYS_LINE)],
