@@ -1047,7 +1047,9 @@ __device__ __forceinline__ void lane_init(Lane& L)
 // 2 (profiles/r06/c4_ab.txt, one call: C4 42.99 -> 38.52 ms, WRITE_SIZE 21.2 -> 2.7 GB per launch):
 // * a lane's rank in the item dispenser by v_mbcnt (lanes_below), not a popcount of
 //   m & ((1 << lane) - 1), whose 64-bit lane mask the compiler hoisted out of the loop and spilled;
-// * the pixel's frame x and y in one register (L.fx = x | y << 16; frames < 65536 wide / high);
+// * the pixel's frame x and y in one register (L.fx = x | y << 16); since the xorshift stream (round 6),
+//   in none: decoded from the item again at each sample start (item_pixel), as is the sample index
+//   (item_sample; C4 scratch 24 -> 8 B per lane);
 // * the pixel's RNG key derived again at each sample start instead of held per lane;
 // * 1/d of every lane's query rebuilt after the shading phase instead of held through it.
 // The brute-force kernels keep their layout (they read the pixel key from the scene's table).
@@ -1055,16 +1057,38 @@ __device__ __forceinline__ unsigned lanes_below(unsigned long long m)
 {
     return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
-template <bool NT>
-__device__ __forceinline__ int lane_fx(const Lane& L)
+// A work item's pixel: item = ((block << log2_chunks) + chunk) * 64 + pixel of the 8x8 block, tile
+// coordinates (px, py), its chunk c, and its frame coordinates (fx, fy; a band set maps tile rows to
+// frame rows).
+template <class ParT>
+__device__ __forceinline__ void item_pixel(unsigned item, const ParT& p, int& px, int& py, int& c, int& fx, int& fy)
 {
-    return NT ? (L.fx & 0xFFFF) : L.fx;
+    const unsigned q = item & 63u, t = item >> 6;
+    c = (int)(t & (unsigned)(p.n_chunks - 1));
+    unsigned by, bx;
+    const unsigned blk = t >> p.log2_chunks;
+    if (p.magic_bx != 0) { // multiply-high division (exact here, make_params checks)
+        by = __umulhi(blk, p.magic_bx);
+        bx = blk - by * (unsigned)p.blocks_x;
+    } else {
+        divmod(blk, (unsigned)p.blocks_x, p.inv_blocks_x, by, bx);
+    }
+    px = (int)bx * 8 + (int)(q & 7);
+    py = (int)by * 8 + (int)(q >> 3);
+    fx = p.x0 + px;
+    fy = p.y0 + py;
+    if (p.band > 0) { // band set: tile row py -> frame row (wave-uniform branch)
+        unsigned bq, br;
+        if (p.band_log2 >= 0) {
+            bq = (unsigned)py >> p.band_log2;
+            br = (unsigned)py & (unsigned)(p.band - 1);
+        } else {
+            divmod((unsigned)py, (unsigned)p.band, p.inv_band, bq, br);
+        }
+        fy = p.y0 + ((int)bq * p.band_stride + p.band_offset) * p.band + (int)br;
+    }
 }
-template <bool NT>
-__device__ __forceinline__ int lane_fy(const Lane& L)
-{
-    return NT ? (int)((unsigned)L.fx >> 16) : L.fy;
-}
+
 // The next sample of the lane's item.  The BVH (NT) kernels hold no register for it: the item's
 // first sample (its chunk, from the item index) plus the samples it finished (samples + misses).
 template <bool NT, class ParT>
@@ -1089,6 +1113,7 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
             p.partial[L.item] = part;
         }
         L.item_open = false;
+        L.ar = L.ag = L.ab = 0.0f; // the next item starts from zero
     }
     const unsigned long long m = __ballot(need);
     if (m) {
@@ -1121,45 +1146,25 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
             if (L.item >= total) {
                 L.active = false;
             } else {
-                // item = ((block << log2_chunks) + chunk) * 64 + pixel of the 8x8 block
-                const unsigned q = L.item & 63u, t = L.item >> 6;
-                const int c = (int)(t & (unsigned)(p.n_chunks - 1));
-                unsigned by, bx;
-                const unsigned blk = t >> p.log2_chunks;
-                if (p.magic_bx != 0) { // multiply-high division (exact here, make_params checks)
-                    by = __umulhi(blk, p.magic_bx);
-                    bx = blk - by * (unsigned)p.blocks_x;
-                } else {
-                    divmod(blk, (unsigned)p.blocks_x, p.inv_blocks_x, by, bx);
-                }
-                const int px = (int)bx * 8 + (q & 7), py = (int)by * 8 + (q >> 3);
+                int px, py, c, fx, fy;
+                item_pixel(L.item, p, px, py, c, fx, fy);
                 if (px < p.w && py < p.h && c * p.chunk < p.spp) {
                     L.item_open = true;
                     const int s0 = c * p.chunk;
                     if (!NT) L.s_next = s0; // (the BVH kernels derive it: item_sample)
                     L.cnt = (unsigned)(min(p.spp, s0 + p.chunk) - s0) << 16; // chunk <= 64
-                    L.ar = L.ag = L.ab = 0.0f;
-                    L.fx = p.x0 + px;
-                    L.fy = p.y0 + py;
-                    if (p.band > 0) { // band set: tile row py -> frame row (wave-uniform branch)
-                        unsigned bq, br;
-                        if (p.band_log2 >= 0) {
-                            bq = (unsigned)py >> p.band_log2;
-                            br = (unsigned)py & (unsigned)(p.band - 1);
-                        } else {
-                            divmod((unsigned)py, (unsigned)p.band, p.inv_band, bq, br);
-                        }
-                        L.fy = p.y0 + ((int)bq * p.band_stride + p.band_offset) * p.band + (int)br;
+                    if (!NT) { // (the BVH kernels decode the item again at each sample start)
+                        L.fx = fx;
+                        L.fy = fy;
                     }
-                    if (NT) L.fx |= L.fy << 16; // one register for both (frames < 65536 wide / high)
                     // the frame width from the launch record (a scene-specialised build's constant
                     // scene leaves it out, so one build serves every frame size)
-                    const unsigned long long px = (unsigned long long)lane_fy<NT>(L) * (unsigned long long)p.scene.width +
-                                                  (unsigned long long)lane_fx<NT>(L);
+                    const unsigned long long pix = (unsigned long long)fy * (unsigned long long)p.scene.width +
+                                                   (unsigned long long)fx;
                     // the brute-force kernels read the key from the scene's table (the same value:
                     // two hash rounds fewer per item open, which runs in most iterations)
-                    if (!NT && p.pkeys) L.pkey = p.pkeys[px];
-                    else if (!NT) L.pkey = rt_rng_pixel_key(p.seed_key, px);
+                    if (!NT && p.pkeys) L.pkey = p.pkeys[pix];
+                    else if (!NT) L.pkey = rt_rng_pixel_key(p.seed_key, pix);
                 }
             }
         }
@@ -1171,11 +1176,15 @@ __device__ __forceinline__ void refill(Lane& L, Sample& S, const ParT& p, const 
         }
     }
     if (L.active && L.item_open && !L.live && L.cnt >= 65536u) {
-        if (NT) // the key from the pixel at every sample start: two registers fewer held
-            L.pkey = rt_rng_pixel_key(p.seed_key, (unsigned long long)lane_fy<NT>(L) * (unsigned long long)p.scene.width +
-                                                      (unsigned long long)lane_fx<NT>(L));
+        int fx = L.fx, fy = L.fy;
+        if (NT) { // the pixel and its key again at every sample start: three registers fewer held
+            int px, py, c;
+            item_pixel(L.item, p, px, py, c, fx, fy);
+            L.pkey = rt_rng_pixel_key(p.seed_key, (unsigned long long)fy * (unsigned long long)p.scene.width +
+                                                      (unsigned long long)fx);
+        }
         S.rng = rt_rng_from_pixel_key(L.pkey, p.sample_base + (unsigned long long)item_sample<NT>(L, p));
-        start_sample<!NT>(cam, lane_fx<NT>(L), lane_fy<NT>(L), S);
+        start_sample<!NT>(cam, fx, fy, S);
         L.live = true;
     }
 }
@@ -1514,8 +1523,9 @@ __global__ void __launch_bounds__(256, WIDTH == 4 ? RT_BVH_WAVES : RT_BVH2_WAVES
                     if (q < p.ray_log_cap) {
                         float4* r = p.ray_log + 3 * (size_t)q;
                         r[0] = make_float4(S.o.x, S.o.y, S.o.z, __int_as_float(S.prev));
-                        r[1] = make_float4(S.d.x, S.d.y, S.d.z,
-                                           __int_as_float(lane_fy<true>(L) * p.scene.width + lane_fx<true>(L)));
+                        int px, py, c, fx, fy;
+                        item_pixel(L.item, p, px, py, c, fx, fy);
+                        r[1] = make_float4(S.d.x, S.d.y, S.d.z, __int_as_float(fy * p.scene.width + fx));
                         r[2] = make_float4(b.t, __int_as_float(b.sg), __int_as_float(S.bounce), 0.0f);
                     }
                 }

@@ -59,10 +59,8 @@ PATCHES = {
                     "        D = (tmin <= fminf(tmax * 1.00000024f, tmax_best)) ? tmin : __builtin_huge_valf();         \\\n")],
     # work items of one wave: the samples of one pixel (chunk-major) instead of one sample of the
     # 64 pixels of an 8x8 block (C4 ray-coherence probe: a wave's primary rays then meet one point)
-    "SAMPLE_MAJOR": [("                const unsigned q = L.item & 63u, t = L.item >> 6;\n"
-                      "                const int c = (int)(t & (unsigned)(p.n_chunks - 1));\n",
-                      "                const unsigned q = (L.item >> p.log2_chunks) & 63u, t = ((L.item >> (p.log2_chunks + 6)) << p.log2_chunks) | (L.item & (unsigned)(p.n_chunks - 1));\n"
-                      "                const int c = (int)(t & (unsigned)(p.n_chunks - 1));\n")],
+    "SAMPLE_MAJOR": [("    const unsigned q = item & 63u, t = item >> 6;\n",
+                      "    const unsigned q = (item >> p.log2_chunks) & 63u, t = ((item >> (p.log2_chunks + 6)) << p.log2_chunks) | (item & (unsigned)(p.n_chunks - 1));\n")],
     # leaf step: a record past the leaf's end is loaded from the leaf's first record instead (same
     # instructions, no spare line): the cost of the spare records' lines
     "NO_SPARE_LINE": [("        r[j][0] = rows[3 * (k + j)];\n"
