@@ -1,5 +1,5 @@
 /*
- * rtcore_rng.h -- the shared, seeded, counter-based random stream of the path tracer.
+ * rtcore_rng.h -- the shared, seeded random stream of the path tracer (keyed by seed, pixel, sample).
  *
  * Why this exists: the reference draws every random number from an unseeded
  * System.Random per worker thread (RaytracerCore/Raytracing/Raytracer.cs:48), so its

@@ -36,7 +36,7 @@ struct Sampler {
 // System.Random of .NET Core 3.1 (the BCL the reference targets, RaytracerCore.csproj:5; not
 // vendored): Knuth's subtractive generator as the BCL implements it, including its second
 // index starting at 21 (so X[n] = X[n-55] - X[n-34] mod int.MaxValue), NextDouble =
-// InternalSample() / int.MaxValue.  Diagnostic only: the shared counter-based stream
+// InternalSample() / int.MaxValue.  Diagnostic only: the shared keyed stream
 // (include/rtcore_rng.h) is the normative one; this one lets the oracle draw the way one
 // reference worker thread does (Raytracer.cs:48, one Random per worker, consumed in pixel order).
 struct NetRandom {
