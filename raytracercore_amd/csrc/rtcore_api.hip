@@ -1720,14 +1720,31 @@ int run_path(rt_scene* s, PathParams& p, unsigned long long* d_rays, hipStream_t
     // order after the previous operation when it ran on another stream (shared scratch)
     if (s->any_op && stream != s->last_stream) HIP_TRY(hipStreamWaitEvent(stream, s->done_ev, 0));
     HIP_TRY(hipMemsetAsync(p.counter, 0, sizeof(unsigned int) * kSplitStride * p.n_split, stream));
-    const int grid = s->n_cu * (s->stats_on ? s->stats_blocks_per_cu : s->blocks_per_cu);
+    int grid = s->n_cu * (s->stats_on ? s->stats_blocks_per_cu : s->blocks_per_cu);
     p.stack_ovf = nullptr;
     if (s->variant >= 4) { // BVH kernels: the stacks' global overflow area
         HIP_TRY(s->stack_ovf.reserve((size_t)grid * 256 * kStackOverflow));
         p.stack_ovf = s->stack_ovf.p;
     }
     const int jit = prepare_jit(s);
-    const int jit_grid = jit ? s->n_cu * s->jit.blocks_per_cu : 0;
+    int jit_grid = jit ? s->n_cu * s->jit.blocks_per_cu : 0;
+    // A small brute-force launch runs fewer blocks per CU.  Its time is a lane's serial chain of
+    // samples (each a few dependent iterations), and an iteration takes as long as the waves sharing
+    // a SIMD make it: with ~2 samples per lane (bounce.txt 256x256 x 16 spp on 8 blocks per CU) the
+    // launch is all tail.  So the grid gives each lane at least kSamplesPerLane samples, up to the
+    // occupancy the kernel allows.  Measured on that launch (profiles/r06/probe_grid.log, kernel ms):
+    // 8 / 6 / 4 / 3 / 2 blocks per CU 0.205 / 0.191 / 0.165 / 0.156-0.161 / 0.163-0.164; the 1080p x 256
+    // spp launch (1,157 samples per lane) stays at the full 8 (16.72-16.75 ms; 6: 17.11).  Which lane
+    // renders an item never changes what it computes.  RTCORE_GRID_BPC caps it (tuning).
+    if ((s->variant >> 1) < 2 && !s->stats_on) {
+        constexpr double kSamplesPerLane = 6.0;
+        const double samples = (double)p.w * (double)p.h * (double)p.spp;
+        int cap = (int)std::ceil(samples / ((double)s->n_cu * 256.0 * kSamplesPerLane));
+        if (const char* e = getenv("RTCORE_GRID_BPC")) cap = atoi(e);
+        cap = std::max(1, cap);
+        if (jit) jit_grid = s->n_cu * std::min(s->jit.blocks_per_cu, cap);
+        else grid = s->n_cu * std::min(s->blocks_per_cu, cap);
+    }
     const int tslot = (int)(s->launches % rt_scene::kTimeRing);
     if (timed) HIP_TRY(hipEventRecord(s->t_start[tslot], stream));
     if (!s->params_h) {
