@@ -1165,3 +1165,23 @@ def test_scene_and_frame_lifecycle_returns_device_memory(rc, scenes):
         round_trip(1 if k < 3 else 0)
     free1, _ = torch.cuda.mem_get_info(0)
     assert free1 >= free0 - (32 << 20), (free0 - free1) / 2**20  # MiB not returned
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["bounce.txt", "die.txt"])
+def test_small_launch_grid_does_not_change_results(rc, scenes, name, monkeypatch):
+    """A small brute-force launch runs fewer blocks per CU (run_path: >= 6 samples per lane); which
+    lane renders an item never changes what it computes, so the full grid (RTCORE_GRID_BPC=8, read
+    per launch) and the capped ones give the same bits."""
+    gpu = rc.GpuRaytracer(scenes[name], 0, size=(256, 256))
+    out = []
+    for bpc in ("8", "3", "1", None):
+        if bpc is None:
+            monkeypatch.delenv("RTCORE_GRID_BPC", raising=False)
+        else:
+            monkeypatch.setenv("RTCORE_GRID_BPC", bpc)
+        out.append(gpu.render_tile(0, 0, 256, 256, 16, seed=3))
+    for r in out[1:]:
+        for a, b in zip(out[0][:3], r[:3]):
+            assert np.array_equal(a, b)
+        assert r[3] == out[0][3]
