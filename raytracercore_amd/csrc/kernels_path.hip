@@ -1505,7 +1505,11 @@ __global__ void __launch_bounds__(256, WIDTH == 4 ? RT_BVH_WAVES : RT_BVH2_WAVES
         const unsigned long long waiting = __ballot(!trav && (L.active || L.live));
         const unsigned long long busy = __ballot(trav);
         if (!waiting && !busy) break;
-        if (!busy || __popcll(waiting) >= p.refill) {
+        // The threshold is at most half the lanes still holding work, so that a wave whose item pool
+        // ran dry does not hold its finished lanes until every query ends (C4 38.24-38.28 -> 38.10-38.15
+        // ms, profiles/r06/ab_refill_adapt.log)
+        const int refill_at = min(p.refill, (__popcll(waiting | busy) + 1) >> 1);
+        if (!busy || __popcll(waiting) >= refill_at) {
             wave_rays += (unsigned)__popcll(__ballot(done)); // one Scene.RayTrace per finished query
             if (done) { // the query finished: the outer records and planes (outside the BVH), then one bounce
                 // (a NaN direction, from a vertex-normal triangle, meets nothing: see path_body).  Here,
