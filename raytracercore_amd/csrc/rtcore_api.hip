@@ -1517,13 +1517,18 @@ PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint6
     // a few chunks per pixel keep the tail of a launch short while each lane still amortises
     // its item fetch over many samples (RTCORE_PATH_CHUNKS overrides the count, for tuning).
     // A launch over fewer pixels than a 1080p frame takes proportionally more chunks per pixel
-    // (up to 8 x the base count: 256 for the brute-force kernels, 512 for the BVH kernels; the
+    // (up to 8 x the base count: 192 for the brute-force kernels, 512 for the BVH kernels; the
     // partial buffer is 16 B x chunks x padded pixels), so that a band set of 1/N of the frame at N x the samples (bench.py on N GPUs)
     // gets items as short as one GPU's whole-frame launch, and with them the same launch tail.
     // The BVH kernels take twice as many (C4 at 64 spp: one sample per item; 16 / 32 / 64 chunks
     // 58.7 / 55.0-55.2 / 53.7 ms): their items start in batched shading phases, so a short item
     // costs little, and the tail of a launch of long, divergent BVH paths shrinks.
-    const int base_chunks = (s->variant >> 1) >= 2 ? 64 : 32;
+    // Brute-force kernels: 24 chunks (round 6, after the xorshift stream; same call, two rounds,
+    // profiles/r06/chunk_sweep3.log, ms per step): C2 16 / 20 / 24 / 28 / 32 chunks 17.12 / 16.86 /
+    // 16.84-16.86 / 16.85-16.87 / 16.98; C3 22.16-22.29 / 21.49-21.50 / 21.42-21.43 / 21.43-21.46 /
+    // 21.86-21.93.  Fewer, longer items (and fewer partials to fold) until the launch tail grows;
+    // 24 chunks leave 8 of the 32 power-of-two chunk slots empty, items the refill skips.
+    const int base_chunks = (s->variant >> 1) >= 2 ? 64 : 24;
     int chunks = base_chunks;
     const double npix = chunk_npix > 0.0 ? chunk_npix : (double)w * (double)h;
     if (npix > 0 && npix < 2073600.0)
