@@ -1563,7 +1563,10 @@ PathParams make_params(rt_scene* s, int x0, int y0, int w, int h, int spp, uint6
     // multiples 1 / 2 / 4 / 8): flat brute force C2 19.54-19.57 / 19.63-19.69 / 20.05 ms, the BVH
     // kernels C4 44.54-44.57 / 44.25-44.28 / 45.0-45.2 / 46.8 ms; grouped C3 27.81 / - / 27.58-27.64.
     const int kernel = s->variant >> 1;
-    int pool_mul = kernel == 0 ? 1 : kernel == 1 ? 4 : 2;
+    // Round 6, with the 24-chunk items (longer items, so fewer per atomic; profiles/r06/pool_sweep2.log):
+    // grouped C3 pool multiples 2 / 4 / 8: 19.93 / 20.36-20.38 / 21.51-21.57 ms; flat C2 1 / 2: 16.27-16.28 /
+    // 16.42-16.49 ms.
+    int pool_mul = kernel == 0 ? 1 : 2;
     if (const char* e = getenv("RTCORE_POOL_MUL")) pool_mul = std::max(1, std::min(64, atoi(e)));
     p.pool = 64;
     while (p.pool < 64 * pool_mul && p.pool < 64 * p.n_chunks) p.pool *= 2;
